@@ -1,0 +1,256 @@
+"""CPU oracle for the dLSM Bloom-filter hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this package, and only as the checker / the timed CPU baseline.
+The product path (``dlsm_amd``) never imports it.
+
+``liboracle.so`` is the plain-C restatement (``bloom_oracle.c``); ``_ref/libref.so``
+is the reference compiled in place (this container only, see ``build_ref.sh``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+u8p = C.POINTER(C.c_uint8)
+u64p = C.POINTER(C.c_uint64)
+
+
+def build(quiet: bool = True) -> None:
+    """Compile liboracle.so (and _ref/libref.so when the reference is mounted)."""
+    out = subprocess.DEVNULL if quiet else None
+    subprocess.run(["make", "-C", _HERE, "liboracle.so"], check=True, stdout=out)
+    subprocess.run(["bash", os.path.join(_HERE, "build_ref.sh")], check=True, stdout=out)
+
+
+def _ptr(a, t=u8p):
+    if a is None:
+        return None
+    return a.ctypes.data_as(t)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.orc_hash.restype = C.c_uint32
+        L.orc_hash.argtypes = [u8p, C.c_size_t, C.c_uint32]
+        L.orc_bloom_hash.restype = C.c_uint32
+        L.orc_bloom_hash.argtypes = [u8p, C.c_size_t]
+        L.orc_full_num_probes.argtypes = [C.c_int]
+        L.orc_legacy_num_probes.argtypes = [C.c_int]
+        L.orc_full_filter_bytes.restype = C.c_uint64
+        L.orc_full_filter_bytes.argtypes = [C.c_uint64, C.c_int, C.POINTER(C.c_uint32)]
+        L.orc_full_dedup_count.restype = C.c_uint64
+        L.orc_full_dedup_count.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64]
+        L.orc_full_build.restype = C.c_int64
+        L.orc_full_build.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, C.c_int, u8p, C.c_uint64]
+        L.orc_full_reader_parse.argtypes = [u8p, C.c_uint64, C.POINTER(C.c_int),
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
+        L.orc_full_key_may_match.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t]
+        L.orc_legacy_filter_bytes.restype = C.c_uint64
+        L.orc_legacy_filter_bytes.argtypes = [C.c_uint64, C.c_int]
+        L.orc_legacy_build.restype = C.c_int64
+        L.orc_legacy_build.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, C.c_int, u8p, C.c_uint64]
+        L.orc_legacy_key_may_match.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t]
+        L.orc_gen_keys_arith.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, u8p]
+        L.orc_gen_values_mt.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, u64p]
+        L.orc_gen_keys_from_values.argtypes = [u64p, C.c_uint64, C.c_int, u8p]
+        L.orc_fnv1a64.restype = C.c_uint64
+        L.orc_fnv1a64.argtypes = [u8p, C.c_uint64]
+        L.orc_full_build_many.argtypes = [C.POINTER(u8p), u64p, C.c_uint32, C.c_int, C.c_int,
+                                          C.POINTER(u8p), u64p, C.POINTER(C.c_int64), C.c_int]
+        L.orc_full_probe_many.argtypes = [C.POINTER(u8p), u64p, C.c_int, u8p, C.c_uint32,
+                                          C.c_uint64, u8p, C.c_int]
+        L.orc_full_probe_var.argtypes = [C.POINTER(u8p), u64p, C.c_int, u8p, u64p, C.c_uint32,
+                                         C.c_uint64, u8p]
+        L.orc_legacy_probe.argtypes = [u8p, C.c_uint64, u8p, u64p, C.c_uint32, C.c_uint64, u8p]
+        L.orc_crc32c_extend.restype = C.c_uint32
+        L.orc_crc32c_extend.argtypes = [C.c_uint32, u8p, C.c_uint64]
+        L.orc_crc32c_mask.restype = C.c_uint32
+        L.orc_crc32c_mask.argtypes = [C.c_uint32]
+        _LIB = L
+    return _LIB
+
+
+def ref_lib():
+    """The reference compiled in place, or None (GPU box / reference absent)."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(_HERE, "_ref", "libref.so")
+        if not os.path.exists(path):
+            return None
+        R = C.CDLL(path)
+        cp = C.c_char_p
+        R.ref_hash.restype = C.c_uint32
+        R.ref_hash.argtypes = [cp, C.c_size_t, C.c_uint32]
+        R.ref_bloom_hash.restype = C.c_uint32
+        R.ref_bloom_hash.argtypes = [cp, C.c_size_t]
+        R.ref_legacy_create.restype = C.c_int64
+        R.ref_legacy_create.argtypes = [cp, u64p, C.c_int, C.c_int, C.c_void_p]
+        R.ref_legacy_may_match.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
+        R.ref_full_build.restype = C.c_int64
+        R.ref_full_build.argtypes = [cp, u64p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
+        R.ref_full_may_match.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
+        _REF = R
+    return _REF
+
+
+# ---------------------------------------------------------------------------
+# Key sets.  A key set is (bytes: uint8[...], offsets: uint64[n+1] | None,
+# stride: int, n: int).  Fixed-stride sets have offsets=None.
+# ---------------------------------------------------------------------------
+
+def dbbench_keys(first: int, step: int, n: int, key_size: int = 20) -> np.ndarray:
+    """Keys v = first + i*step (db_bench GenerateKeyFromInt), packed [n, key_size]."""
+    out = np.empty(n * key_size, dtype=np.uint8)
+    lib().orc_gen_keys_arith(first, step, n, key_size, _ptr(out))
+    return out
+
+
+def mt_values(seed: int, modulus: int, n: int) -> np.ndarray:
+    out = np.empty(n, dtype=np.uint64)
+    lib().orc_gen_values_mt(seed, modulus, n, _ptr(out, u64p))
+    return out
+
+
+def keys_from_values(v: np.ndarray, key_size: int = 20) -> np.ndarray:
+    v = np.ascontiguousarray(v, dtype=np.uint64)
+    out = np.empty(v.size * key_size, dtype=np.uint8)
+    lib().orc_gen_keys_from_values(_ptr(v, u64p), v.size, key_size, _ptr(out))
+    return out
+
+
+def pack_var(keys: list[bytes]):
+    offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+    if keys:
+        offs[1:] = np.cumsum([len(k) for k in keys])
+    data = np.frombuffer(b"".join(keys) + b"\0", dtype=np.uint8).copy()
+    return data, offs
+
+
+def bloom_hash(key: bytes) -> int:
+    a = np.frombuffer(key + b"\0", dtype=np.uint8)
+    return int(lib().orc_bloom_hash(_ptr(a), len(key)))
+
+
+def hash_seed(key: bytes, seed: int) -> int:
+    a = np.frombuffer(key + b"\0", dtype=np.uint8)
+    return int(lib().orc_hash(_ptr(a), len(key), seed))
+
+
+def full_filter_bytes(n_dedup: int, bpk: int = 10):
+    nl = C.c_uint32(0)
+    b = lib().orc_full_filter_bytes(n_dedup, bpk, C.byref(nl))
+    return int(b), int(nl.value)
+
+
+def full_build(keys: np.ndarray, n: int, stride: int = 20, offsets=None, bpk: int = 10) -> bytes:
+    if offsets is None:
+        nd = n
+    else:
+        nd = n
+    cap = full_filter_bytes(nd, bpk)[0]
+    out = np.zeros(cap, dtype=np.uint8)
+    r = lib().orc_full_build(_ptr(keys), _ptr(offsets, u64p), stride, n, bpk, _ptr(out), cap)
+    if r < 0:
+        raise RuntimeError(f"orc_full_build: {r}")
+    return out[:r].tobytes()
+
+
+def full_dedup_count(keys, n, stride=20, offsets=None) -> int:
+    return int(lib().orc_full_dedup_count(_ptr(keys), _ptr(offsets, u64p), stride, n))
+
+
+def full_reader_parse(filt: bytes):
+    a = np.frombuffer(filt + b"\0", dtype=np.uint8)
+    k, L, lg = C.c_int(0), C.c_uint32(0), C.c_int(0)
+    st = lib().orc_full_reader_parse(_ptr(a), len(filt), C.byref(k), C.byref(L), C.byref(lg))
+    return st, k.value, L.value, lg.value
+
+
+def full_probe(filters: list[bytes], keys: np.ndarray, n: int, stride: int = 20,
+               offsets=None, nthreads: int = 1) -> np.ndarray:
+    F = len(filters)
+    fa = [np.frombuffer(f, dtype=np.uint8) for f in filters]
+    fptrs = (u8p * F)(*[_ptr(a) for a in fa])
+    flen = np.array([len(f) for f in filters], dtype=np.uint64)
+    mb = (F + 7) // 8
+    mask = np.zeros(n * mb, dtype=np.uint8)
+    if offsets is None:
+        st = lib().orc_full_probe_many(fptrs, _ptr(flen, u64p), F, _ptr(keys), stride, n,
+                                       _ptr(mask), nthreads)
+    else:
+        st = lib().orc_full_probe_var(fptrs, _ptr(flen, u64p), F, _ptr(keys), _ptr(offsets, u64p),
+                                      stride, n, _ptr(mask))
+    if st:
+        raise RuntimeError(f"orc probe status {st}")
+    return mask
+
+
+def full_key_may_match(filt: bytes, key: bytes) -> int:
+    a = np.frombuffer(filt + b"\0", dtype=np.uint8)
+    k = np.frombuffer(key + b"\0", dtype=np.uint8)
+    return int(lib().orc_full_key_may_match(_ptr(a), len(filt), _ptr(k), len(key)))
+
+
+def legacy_build(keys: np.ndarray, n: int, stride: int = 20, offsets=None, bpk: int = 10) -> bytes:
+    cap = int(lib().orc_legacy_filter_bytes(n, bpk))
+    out = np.zeros(cap, dtype=np.uint8)
+    r = lib().orc_legacy_build(_ptr(keys), _ptr(offsets, u64p), stride, n, bpk, _ptr(out), cap)
+    if r < 0:
+        raise RuntimeError(f"orc_legacy_build: {r}")
+    return out[:r].tobytes()
+
+
+def legacy_probe(filt: bytes, keys: np.ndarray, n: int, stride: int = 20, offsets=None) -> np.ndarray:
+    a = np.frombuffer(filt + b"\0", dtype=np.uint8)
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    lib().orc_legacy_probe(_ptr(a), len(filt), _ptr(keys), _ptr(offsets, u64p), stride, n, _ptr(out))
+    return out[:n]
+
+
+def legacy_key_may_match(filt: bytes, key: bytes) -> int:
+    a = np.frombuffer(filt + b"\0", dtype=np.uint8)
+    k = np.frombuffer(key + b"\0", dtype=np.uint8)
+    return int(lib().orc_legacy_key_may_match(_ptr(a), len(filt), _ptr(k), len(key)))
+
+
+def fnv1a64(data) -> int:
+    a = np.frombuffer(bytes(data) + b"\0", dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    n = len(data) if not isinstance(data, np.ndarray) else data.size
+    return int(lib().orc_fnv1a64(_ptr(np.ascontiguousarray(a, dtype=np.uint8)), n))
+
+
+def crc32c(data: bytes, init: int = 0) -> int:
+    a = np.frombuffer(data + b"\0", dtype=np.uint8)
+    return int(lib().orc_crc32c_extend(init, _ptr(a), len(data)))
+
+
+def crc32c_mask(crc: int) -> int:
+    return int(lib().orc_crc32c_mask(crc))
+
+
+def full_build_many(tables: list[np.ndarray], ns: list[int], stride: int, bpk: int,
+                    nthreads: int):
+    """CPU baseline: build len(tables) full filters on `nthreads` threads."""
+    T = len(tables)
+    caps = np.array([full_filter_bytes(n, bpk)[0] for n in ns], dtype=np.uint64)
+    outs = [np.zeros(int(c), dtype=np.uint8) for c in caps]
+    kp = (u8p * T)(*[_ptr(t) for t in tables])
+    op = (u8p * T)(*[_ptr(o) for o in outs])
+    nn = np.array(ns, dtype=np.uint64)
+    lens = (C.c_int64 * T)()
+    lib().orc_full_build_many(kp, _ptr(nn, u64p), stride, T, bpk, op, _ptr(caps, u64p), lens,
+                              nthreads)
+    return [o[: lens[i]].tobytes() for i, o in enumerate(outs)]
