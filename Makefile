@@ -1,0 +1,37 @@
+# Build the MI355X (gfx950) Bloom-filter library and the CPU oracle.
+#   make            -> dlsm_amd/lib/libdlsm_bloom.so + oracle/liboracle.so
+#   make oracle-ref -> oracle/_ref/libref.so (build container only)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
+SRC := dlsm_amd/csrc/bloom_kernels.hip dlsm_amd/csrc/bloom_capi.hip
+HDR := dlsm_amd/csrc/bloom_math.h dlsm_amd/csrc/bloom_internal.h include/dlsm_bloom.h
+LIB := dlsm_amd/lib/libdlsm_bloom.so
+OBJ := $(patsubst dlsm_amd/csrc/%.hip,build/%.o,$(SRC))
+
+all: $(LIB) oracle
+
+build/%.o: dlsm_amd/csrc/%.hip $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p dlsm_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJ) -o $@
+
+oracle:
+	$(MAKE) -C oracle liboracle.so
+
+oracle-ref:
+	$(MAKE) -C oracle ref
+
+asm: dlsm_amd/csrc/bloom_kernels.hip $(HDR)
+	@mkdir -p build/asm
+	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $< -o build/asm/bloom_kernels.s \
+	  -Rpass-analysis=kernel-resource-usage 2> build/asm/resource_usage.txt || true
+
+clean:
+	rm -rf build dlsm_amd/lib
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle oracle-ref asm clean

@@ -1,0 +1,260 @@
+"""dlsm_amd -- MI355X-native SSTable Bloom-filter engine for dLSM.
+
+Python face of the C ABI (``include/dlsm_bloom.h``).  The compute path is the
+hand-written gfx950 HIP library ``dlsm_amd/lib/libdlsm_bloom.so``; this package
+only marshals buffers (numpy arrays for host memory, torch tensors for device
+memory) and mirrors the reference's class surface:
+
+* :class:`FullFilterBlockBuilder` / :class:`FullFilterBlockReader`
+  (table/full_filter_block.h:33-94)
+* :class:`BloomFilterPolicy` (include/TimberSaw/filter_policy.h:31-71,
+  util/bloom.cc)
+
+There is no CPU fallback: without the HIP library every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as _L
+from ._lib import DlsmError, check, dlsm_build_job, dlsm_keyset
+
+__all__ = [
+    "Keys", "Context", "FilterSet", "DlsmError", "device_available", "bloom_hash",
+    "full_size", "legacy_size", "full_parse", "FullFilterBlockBuilder",
+    "FullFilterBlockReader", "BloomFilterPolicy", "PATH_AUTO", "PATH_DIRECT", "PATH_SLICED",
+]
+
+PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
+
+
+def lib():
+    return _L._lib()
+
+
+def device_available() -> bool:
+    n = C.c_int(0)
+    try:
+        lib().dlsm_device_count(C.byref(n))
+    except OSError:
+        return False
+    return n.value > 0
+
+
+def bloom_hash(key: bytes) -> int:
+    """BloomHash (include/TimberSaw/filter_policy.h:26-28), host side."""
+    b = C.create_string_buffer(bytes(key), len(key) + 1)
+    return int(lib().dlsm_bloom_hash(b, len(key)))
+
+
+def full_size(n_dedup: int, bits_per_key: int = 10):
+    L = C.c_uint32(0)
+    nb = C.c_uint64(0)
+    check(lib().dlsm_bloom_full_size(n_dedup, bits_per_key, C.byref(L), C.byref(nb)))
+    return int(nb.value), int(L.value)
+
+
+def legacy_size(n: int, bits_per_key: int = 10) -> int:
+    nb = C.c_uint64(0)
+    check(lib().dlsm_bloom_legacy_size(n, bits_per_key, C.byref(nb)))
+    return int(nb.value)
+
+
+def full_parse(filt: bytes):
+    """(status, num_probes, num_lines, log2_line) -- FullFilterBlockReader ctor."""
+    b = C.create_string_buffer(bytes(filt), max(len(filt), 1))
+    k, L, lg = C.c_int(0), C.c_uint32(0), C.c_int(0)
+    st = lib().dlsm_bloom_full_parse(b, len(filt), C.byref(k), C.byref(L), C.byref(lg))
+    return st, k.value, L.value, lg.value
+
+
+def _ptr(x) -> Optional[int]:
+    """Address of a numpy array or torch tensor (host or device)."""
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    return int(x.data_ptr())
+
+
+@dataclass
+class Keys:
+    """A packed key set: ``data`` (uint8) + ``offsets`` (uint64[n+1]) or fixed ``key_len``.
+
+    ``data``/``offsets`` are numpy arrays (host) or torch tensors (device)."""
+    data: object
+    n: int
+    key_len: int = 20
+    offsets: object = None
+
+    def c(self) -> dlsm_keyset:
+        return dlsm_keyset(_ptr(self.data), _ptr(self.offsets), self.key_len, 0, self.n)
+
+    @staticmethod
+    def pack(keys: Sequence[bytes]) -> "Keys":
+        offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+        if keys:
+            offs[1:] = np.cumsum([len(k) for k in keys])
+        data = np.frombuffer(b"".join(keys) + b"\0" * 16, dtype=np.uint8).copy()
+        return Keys(data, len(keys), 0, offs)
+
+
+class FilterSet:
+    """F parsed full filters resident on one device (FullFilterBlockReader state)."""
+
+    def __init__(self, ctx: "Context", filters, on_device: bool = False):
+        self.ctx = ctx
+        F = len(filters)
+        if on_device:
+            ptrs = [_ptr(f) for f in filters]
+            lens = [int(f.numel()) for f in filters]
+            self._keep = list(filters)
+        else:
+            arrs = [np.frombuffer(bytes(f), dtype=np.uint8) for f in filters]
+            ptrs = [a.ctypes.data for a in arrs]
+            lens = [a.size for a in arrs]
+            self._keep = arrs
+        self.n_filters = F
+        self.lens = lens
+        h = C.c_void_p()
+        pa = (C.c_void_p * F)(*ptrs)
+        la = (C.c_uint64 * F)(*lens)
+        check(lib().dlsm_filterset_create(ctx.h, pa, la, F, 1 if on_device else 0, C.byref(h)),
+              "filterset_create")
+        self.h = h
+        self._keep = None
+
+    @property
+    def mask_bytes(self) -> int:
+        return (self.n_filters + 7) // 8
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dlsm_filterset_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One device + one HIP stream + workspace (``dlsm_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().dlsm_ctx_create(device, C.byref(h)), "ctx_create")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dlsm_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing -----------------------------------------------------------
+    def sync(self):
+        check(lib().dlsm_ctx_sync(self.h), "sync")
+
+    def set_path(self, path: int):
+        check(lib().dlsm_ctx_set_path(self.h, path), "set_path")
+
+    def set_stream(self, stream=None):
+        """Run on a torch.cuda.Stream (or its raw handle); None = own stream."""
+        raw = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        check(lib().dlsm_ctx_set_stream(self.h, raw), "set_stream")
+
+    @property
+    def stream_handle(self) -> int:
+        return int(lib().dlsm_ctx_stream(self.h) or 0)
+
+    def reserve(self, max_keys: int, max_jobs: int):
+        check(lib().dlsm_ctx_reserve(self.h, max_keys, max_jobs), "reserve")
+
+    # -- full filter build --------------------------------------------------
+    @staticmethod
+    def _jobs(tables: Sequence[Keys], outs, caps):
+        n = len(tables)
+        arr = (dlsm_build_job * max(n, 1))()
+        for j, t in enumerate(tables):
+            arr[j].keys = t.c()
+            arr[j].out = _ptr(outs[j])
+            arr[j].out_cap = caps[j]
+        return arr
+
+    def full_build(self, tables: Sequence[Keys], bits_per_key: int = 10, caps=None) -> list:
+        """Host keys -> host filter bytes (synchronous).  One filter per table."""
+        n = len(tables)
+        if caps is None:
+            caps = [full_size(t.n, bits_per_key)[0] for t in tables]
+        outs = [np.zeros(max(c, 1), dtype=np.uint8) for c in caps]
+        jobs = self._jobs(tables, outs, caps)
+        lens = (C.c_uint64 * max(n, 1))()
+        check(lib().dlsm_bloom_full_build(self.h, jobs, n, bits_per_key, lens), "full_build")
+        return [outs[j][: lens[j]].tobytes() for j in range(n)]
+
+    def full_build_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
+        """Device keys (torch tensors) -> device slots; asynchronous on this ctx's stream."""
+        caps = [int(o.numel()) for o in outs]
+        jobs = self._jobs(tables, outs, caps)
+        check(lib().dlsm_bloom_full_build_dev(self.h, jobs, len(tables), bits_per_key,
+                                              _ptr(out_lens)), "full_build_dev")
+
+    # -- full filter probe --------------------------------------------------
+    def filterset(self, filters, on_device: bool = False) -> FilterSet:
+        return FilterSet(self, filters, on_device)
+
+    def full_probe(self, fs: FilterSet, keys: Keys) -> np.ndarray:
+        mask = np.zeros(max(keys.n * fs.mask_bytes, 1), dtype=np.uint8)
+        ks = keys.c()
+        check(lib().dlsm_bloom_full_probe(self.h, fs.h, C.byref(ks), mask.ctypes.data), "full_probe")
+        return mask[: keys.n * fs.mask_bytes]
+
+    def full_probe_dev(self, fs: FilterSet, keys: Keys, mask):
+        ks = keys.c()
+        check(lib().dlsm_bloom_full_probe_dev(self.h, fs.h, C.byref(ks), _ptr(mask)),
+              "full_probe_dev")
+
+    # -- legacy FilterPolicy format -----------------------------------------
+    def legacy_build(self, tables: Sequence[Keys], bits_per_key: int = 10) -> list:
+        n = len(tables)
+        caps = [legacy_size(t.n, bits_per_key) for t in tables]
+        outs = [np.zeros(c, dtype=np.uint8) for c in caps]
+        jobs = self._jobs(tables, outs, caps)
+        lens = (C.c_uint64 * max(n, 1))()
+        check(lib().dlsm_bloom_legacy_build(self.h, jobs, n, bits_per_key, lens), "legacy_build")
+        return [outs[j][: lens[j]].tobytes() for j in range(n)]
+
+    def legacy_build_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
+        caps = [int(o.numel()) for o in outs]
+        jobs = self._jobs(tables, outs, caps)
+        check(lib().dlsm_bloom_legacy_build_dev(self.h, jobs, len(tables), bits_per_key,
+                                                _ptr(out_lens)), "legacy_build_dev")
+
+    def legacy_probe(self, filt: bytes, keys: Keys) -> np.ndarray:
+        fa = np.frombuffer(bytes(filt) + b"\0", dtype=np.uint8)
+        out = np.zeros(max(keys.n, 1), dtype=np.uint8)
+        ks = keys.c()
+        check(lib().dlsm_bloom_legacy_probe(self.h, fa.ctypes.data if len(filt) else None, len(filt),
+                                            C.byref(ks), out.ctypes.data), "legacy_probe")
+        return out[: keys.n]
+
+    def legacy_probe_dev(self, filt_dev, length: int, keys: Keys, out):
+        ks = keys.c()
+        check(lib().dlsm_bloom_legacy_probe_dev(self.h, _ptr(filt_dev), length, C.byref(ks),
+                                                _ptr(out)), "legacy_probe_dev")
+
+
+from .filter_block import BloomFilterPolicy, FullFilterBlockBuilder, FullFilterBlockReader  # noqa: E402

@@ -1,0 +1,97 @@
+"""ctypes binding of the C ABI in include/dlsm_bloom.h.
+
+Loads the in-tree gfx950 library ``dlsm_amd/lib/libdlsm_bloom.so`` (built by
+``make`` / ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdlsm_bloom.so")
+
+DLSM_OK = 0
+DLSM_E_ARG = -1
+DLSM_E_CAPACITY = -2
+DLSM_E_CORRUPT = -3
+DLSM_E_DEVICE = -4
+DLSM_E_NOMEM = -5
+
+
+class dlsm_keyset(C.Structure):
+    _fields_ = [("bytes", C.c_void_p), ("offsets", C.c_void_p), ("key_len", C.c_uint32),
+                ("reserved", C.c_uint32), ("n", C.c_uint64)]
+
+
+class dlsm_build_job(C.Structure):
+    _fields_ = [("keys", dlsm_keyset), ("out", C.c_void_p), ("out_cap", C.c_uint64)]
+
+
+class DlsmError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = _lib().dlsm_strerror(status).decode() if _LIB is not None else str(status)
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+# Exported symbols and their signatures: (name, restype, argtypes).
+_VP = C.c_void_p
+_U64P = C.POINTER(C.c_uint64)
+SIGNATURES = [
+    ("dlsm_strerror", C.c_char_p, [C.c_int]),
+    ("dlsm_abi_version", C.c_int, []),
+    ("dlsm_bloom_hash", C.c_uint32, [_VP, C.c_size_t]),
+    ("dlsm_bloom_full_num_probes", C.c_int, [C.c_int]),
+    ("dlsm_bloom_full_size", C.c_int, [C.c_uint64, C.c_int, C.POINTER(C.c_uint32), _U64P]),
+    ("dlsm_bloom_legacy_size", C.c_int, [C.c_uint64, C.c_int, _U64P]),
+    ("dlsm_bloom_full_parse", C.c_int, [_VP, C.c_uint64, C.POINTER(C.c_int),
+                                        C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
+    ("dlsm_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("dlsm_ctx_create", C.c_int, [C.c_int, C.POINTER(_VP)]),
+    ("dlsm_ctx_destroy", C.c_int, [_VP]),
+    ("dlsm_ctx_set_stream", C.c_int, [_VP, _VP]),
+    ("dlsm_ctx_stream", _VP, [_VP]),
+    ("dlsm_ctx_sync", C.c_int, [_VP]),
+    ("dlsm_ctx_reserve", C.c_int, [_VP, C.c_uint64, C.c_uint32]),
+    ("dlsm_ctx_set_path", C.c_int, [_VP, C.c_int]),
+    ("dlsm_host_register", C.c_int, [_VP, C.c_size_t]),
+    ("dlsm_host_unregister", C.c_int, [_VP]),
+    ("dlsm_bloom_full_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
+    ("dlsm_bloom_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
+    ("dlsm_filterset_create", C.c_int, [_VP, C.POINTER(_VP), _U64P, C.c_int, C.c_int,
+                                        C.POINTER(_VP)]),
+    ("dlsm_filterset_destroy", C.c_int, [_VP]),
+    ("dlsm_filterset_size", C.c_int, [_VP, C.POINTER(C.c_int), _U64P]),
+    ("dlsm_bloom_full_probe_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_full_probe", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_legacy_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
+    ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
+    ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_legacy_probe", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
+]
+
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"dlsm_amd: HIP library not built ({LIB_PATH} missing); run `make` or "
+                "__graft_entry__.build() -- there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def check(status: int, what: str = "") -> int:
+    if status != DLSM_OK:
+        raise DlsmError(status, what)
+    return status

@@ -1,0 +1,794 @@
+// dlsm_amd/csrc/bloom_capi.hip -- the C ABI (include/dlsm_bloom.h): contexts,
+// device workspace, job set-up, and the host-buffer (staged) call variants.
+// Kernels live in bloom_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/dlsm_bloom.h"
+#include "bloom_internal.h"
+
+using namespace dlsm;
+
+namespace {
+
+int from_hip(hipError_t e) {
+  if (e == hipSuccess) return DLSM_OK;
+  if (e == hipErrorOutOfMemory) return DLSM_E_NOMEM;
+  return DLSM_E_DEVICE;
+}
+
+#define DLSM_TRY(expr)                       \
+  do {                                       \
+    hipError_t _e = (expr);                  \
+    if (_e != hipSuccess) return from_hip(_e); \
+  } while (0)
+
+#define DLSM_CHECK(expr)         \
+  do {                           \
+    int _s = (expr);             \
+    if (_s != DLSM_OK) return _s; \
+  } while (0)
+
+// Growable device buffer (never shrinks; freed with the context).
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;  // elements
+  int ensure(size_t n) {
+    if (n <= cap && p) return DLSM_OK;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = std::max<size_t>(n, 1);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      return from_hip(e);
+    }
+    cap = want;
+    return DLSM_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+uint32_t ceil_div_u32(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
+
+}  // namespace
+
+struct dlsm_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int path = 0;
+  // build workspace
+  DevBuf<uint32_t> entries;
+  DevBuf<uint32_t> tab;
+  DevBuf<FullJobDev> jobs;
+  DevBuf<uint32_t> starts;  // chunk0s | slice0s
+  DevBuf<JobState> state;
+  DevBuf<LegacyJobDev> ljobs;
+  DevBuf<uint64_t> lstarts;
+  // probe workspace
+  DevBuf<uint16_t> pos;
+  DevBuf<uint8_t> smask;
+  // host-API staging
+  DevBuf<uint8_t> st_keys;
+  DevBuf<uint64_t> st_offs;
+  DevBuf<uint8_t> st_out;
+  DevBuf<uint64_t> st_len;
+  DevBuf<uint8_t> st_filter;
+};
+
+struct dlsm_filterset {
+  int device = 0;
+  int F = 0;
+  uint8_t* blob = nullptr;
+  uint64_t blob_bytes = 0;
+  FilterDev* d_filters = nullptr;
+  std::vector<FilterDev> h;
+  uint64_t* stacked = nullptr;  // L*64 u64 words when stackable
+  uint32_t L = 0, magic = 0;
+  int k = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int validate_keyset(const dlsm_keyset& k) {
+  if (k.n == 0) return DLSM_OK;
+  if (!k.bytes) return DLSM_E_ARG;
+  if (!k.offsets && k.key_len == 0) {
+    // zero-length fixed keys are legal (every key is the empty string)
+    return DLSM_OK;
+  }
+  return DLSM_OK;
+}
+
+KeyDesc to_desc(const dlsm_keyset& k) {
+  KeyDesc d;
+  d.bytes = k.bytes;
+  d.offsets = k.offsets;
+  d.n = k.n;
+  d.key_len = k.key_len;
+  d.pad = 0;
+  return d;
+}
+
+bool is_k20(const dlsm_keyset& k) {
+  return k.offsets == nullptr && k.key_len == 20 && (k.n == 0 || aligned(k.bytes, 4));
+}
+
+// Slice width for the sliced build: the smallest 2^lgR (lgR in [9, 11]) that
+// keeps every job at <= kMaxSlices slices.  Returns -1 if none fits.
+int choose_build_lgR(const std::vector<uint32_t>& Ls) {
+  for (int lg = 9; lg <= 11; lg++) {
+    bool ok = true;
+    for (uint32_t L : Ls)
+      if (((static_cast<uint64_t>(L) + (1u << lg) - 1) >> lg) > kMaxSlices) ok = false;
+    if (ok) return lg;
+  }
+  return -1;
+}
+
+// FullFilterBlockReader ctor checks (table/full_filter_block.cc:186-252) on the
+// filter's 5-byte tail and total length.
+int parse_tail(const uint8_t* tail, uint64_t len64, int* k_out, uint32_t* L_out, int* lg_out) {
+  if (len64 < 5 || len64 > 0xffffffffull) return DLSM_E_CORRUPT;
+  const int k = static_cast<int>(static_cast<int8_t>(tail[0]));
+  if (k < 1) return DLSM_E_CORRUPT;  // the reference exit(1)s
+  const uint32_t len = static_cast<uint32_t>(len64) - 5;
+  const uint32_t L = uint32_t(tail[1]) | (uint32_t(tail[2]) << 8) | (uint32_t(tail[3]) << 16) |
+                     (uint32_t(tail[4]) << 24);
+  int lg;
+  if (L * kCacheLineBytes == len) {
+    // common case; L == 0 (empty filter) would make KeyMayMatch divide by 0,
+    // and a wrapped product would index past the filter
+    if (L == 0 || static_cast<uint64_t>(L) * kCacheLineBytes != len) return DLSM_E_CORRUPT;
+    lg = 6;
+  } else if (L == 0 || len % L != 0) {
+    return DLSM_E_CORRUPT;  // the reference exit(1)s
+  } else {
+    lg = 0;  // log2_cache_line_size_ keeps its initialiser (full_filter_block.h:85)
+  }
+  *k_out = k;
+  *L_out = L;
+  *lg_out = lg;
+  return DLSM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dlsm_strerror(int status) {
+  switch (status) {
+    case DLSM_OK: return "ok";
+    case DLSM_E_ARG: return "invalid argument";
+    case DLSM_E_CAPACITY: return "output slot too small";
+    case DLSM_E_CORRUPT: return "corrupt bloom filter";
+    case DLSM_E_DEVICE: return "HIP device error";
+    case DLSM_E_NOMEM: return "device out of memory";
+    default: return "unknown status";
+  }
+}
+
+int dlsm_abi_version(void) { return DLSM_BLOOM_ABI_VERSION; }
+
+uint32_t dlsm_bloom_hash(const void* key, size_t n) {
+  return bloom_hash_host(static_cast<const uint8_t*>(key), n);
+}
+
+int dlsm_bloom_full_num_probes(int bits_per_key) { return full_num_probes(bits_per_key); }
+
+int dlsm_bloom_full_size(uint64_t n_dedup, int bits_per_key, uint32_t* num_lines,
+                         uint64_t* nbytes) {
+  uint32_t tb;
+  const uint32_t L = full_num_lines(n_dedup, bits_per_key, &tb);
+  if (num_lines) *num_lines = L;
+  if (nbytes) *nbytes = static_cast<uint64_t>(tb / 8u) + 5u;
+  return DLSM_OK;
+}
+
+int dlsm_bloom_legacy_size(uint64_t n, int bits_per_key, uint64_t* nbytes) {
+  if (nbytes) *nbytes = legacy_bits(n, bits_per_key) / 8 + 1;
+  return DLSM_OK;
+}
+
+int dlsm_bloom_full_parse(const uint8_t* f, uint64_t len64, int* num_probes, uint32_t* num_lines,
+                          int* log2_line) {
+  if (!f || len64 < 5) return DLSM_E_CORRUPT;
+  int k, lg;
+  uint32_t L;
+  DLSM_CHECK(parse_tail(f + len64 - 5, len64, &k, &L, &lg));
+  if (num_probes) *num_probes = k;
+  if (num_lines) *num_lines = L;
+  if (log2_line) *log2_line = lg;
+  return DLSM_OK;
+}
+
+int dlsm_device_count(int* n) {
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) c = 0;
+  if (n) *n = c;
+  return e == hipSuccess ? DLSM_OK : from_hip(e);
+}
+
+int dlsm_ctx_create(int device, dlsm_ctx** out) {
+  if (!out) return DLSM_E_ARG;
+  *out = nullptr;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) return DLSM_E_DEVICE;
+  DeviceGuard g(device);
+  dlsm_ctx* ctx = new (std::nothrow) dlsm_ctx();
+  if (!ctx) return DLSM_E_NOMEM;
+  ctx->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete ctx;
+    return from_hip(e);
+  }
+  ctx->stream = ctx->own;
+  *out = ctx;
+  return DLSM_OK;
+}
+
+int dlsm_ctx_destroy(dlsm_ctx* ctx) {
+  if (!ctx) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  ctx->entries.release();
+  ctx->tab.release();
+  ctx->jobs.release();
+  ctx->starts.release();
+  ctx->state.release();
+  ctx->ljobs.release();
+  ctx->lstarts.release();
+  ctx->pos.release();
+  ctx->smask.release();
+  ctx->st_keys.release();
+  ctx->st_offs.release();
+  ctx->st_out.release();
+  ctx->st_len.release();
+  ctx->st_filter.release();
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+  return DLSM_OK;
+}
+
+int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* s) {
+  if (!ctx) return DLSM_E_ARG;
+  ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
+  return DLSM_OK;
+}
+
+void* dlsm_ctx_stream(dlsm_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int dlsm_ctx_sync(dlsm_ctx* ctx) {
+  if (!ctx) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  return DLSM_OK;
+}
+
+int dlsm_ctx_set_path(dlsm_ctx* ctx, int path) {
+  if (!ctx || path < 0 || path > 2) return DLSM_E_ARG;
+  ctx->path = path;
+  return DLSM_OK;
+}
+
+int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
+  if (!ctx) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  DLSM_CHECK(ctx->entries.ensure(max_keys));
+  DLSM_CHECK(ctx->pos.ensure(max_keys));
+  DLSM_CHECK(ctx->smask.ensure(max_keys));
+  const uint64_t chunks = (max_keys + kBuildChunk - 1) / kBuildChunk + max_jobs;
+  DLSM_CHECK(ctx->tab.ensure(chunks * (kMaxSlices + 1)));
+  DLSM_CHECK(ctx->jobs.ensure(max_jobs));
+  DLSM_CHECK(ctx->starts.ensure(2 * (max_jobs + 1)));
+  DLSM_CHECK(ctx->state.ensure(max_jobs));
+  return DLSM_OK;
+}
+
+int dlsm_host_register(void* p, size_t len) {
+  if (!p || !len) return DLSM_E_ARG;
+  DLSM_TRY(hipHostRegister(p, len, hipHostRegisterDefault));
+  return DLSM_OK;
+}
+
+int dlsm_host_unregister(void* p) {
+  if (!p) return DLSM_E_ARG;
+  DLSM_TRY(hipHostUnregister(p));
+  return DLSM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Full filter build
+// ---------------------------------------------------------------------------
+int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                              int bits_per_key, uint64_t* out_len_dev) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  const int k = full_num_probes(bits_per_key);
+  std::vector<uint32_t> Ls(n_jobs);
+  bool all_k20 = true, sliced_ok = ctx->path != 1;
+  for (int j = 0; j < n_jobs; j++) {
+    const dlsm_build_job& b = jobs[j];
+    DLSM_CHECK(validate_keyset(b.keys));
+    if (!b.out || !aligned(b.out, 16)) return DLSM_E_ARG;
+    if (b.keys.n > 0xffffffffull * kBuildChunk) return DLSM_E_ARG;
+    Ls[j] = full_num_lines(b.keys.n, bits_per_key, nullptr);
+    all_k20 = all_k20 && is_k20(b.keys);
+  }
+  int lgR = choose_build_lgR(Ls);
+  if (lgR < 0) sliced_ok = false;
+  if (ctx->path == 2 && !sliced_ok) return DLSM_E_ARG;
+  const int mode = all_k20 ? KM_K20 : KM_GENERIC;
+
+  std::vector<FullJobDev> hj(n_jobs);
+  std::vector<uint32_t> starts(2 * n_jobs);
+  uint64_t entry = 0, tabw = 0;
+  uint32_t chunk = 0, slice = 0;
+  for (int j = 0; j < n_jobs; j++) {
+    const dlsm_build_job& b = jobs[j];
+    FullJobDev& d = hj[j];
+    d.keys = to_desc(b.keys);
+    d.out = b.out;
+    d.out_cap = b.out_cap;
+    d.out_len = out_len_dev + j;
+    d.entry0 = entry;
+    d.n_chunks = ceil_div_u32(b.keys.n, kBuildChunk);
+    d.chunk0 = chunk;
+    d.L_spec = Ls[j];
+    d.magic_spec = Ls[j] ? fastmod_magic(Ls[j]) : 0;
+    d.n_slices = sliced_ok ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], 1ull << lgR)) : 1;
+    d.slice0 = slice;
+    d.tab0 = tabw;
+    d.k = k;
+    d.bpk = bits_per_key;
+    starts[j] = chunk;
+    starts[n_jobs + j] = slice;
+    entry += b.keys.n;
+    chunk += d.n_chunks;
+    slice += d.n_slices;
+    tabw += static_cast<uint64_t>(d.n_slices + 1) * d.n_chunks;
+  }
+  hipStream_t s = ctx->stream;
+  DLSM_CHECK(ctx->jobs.ensure(n_jobs));
+  DLSM_CHECK(ctx->starts.ensure(2 * n_jobs));
+  DLSM_CHECK(ctx->state.ensure(n_jobs));
+  DLSM_TRY(hipMemcpyAsync(ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs,
+                          hipMemcpyHostToDevice, s));
+  DLSM_TRY(hipMemcpyAsync(ctx->starts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs,
+                          hipMemcpyHostToDevice, s));
+  DLSM_TRY(hipMemsetAsync(ctx->state.p, 0, sizeof(JobState) * n_jobs, s));
+  const uint32_t* chunk0s = ctx->starts.p;
+  const uint32_t* slice0s = ctx->starts.p + n_jobs;
+  if (sliced_ok) {
+    DLSM_CHECK(ctx->entries.ensure(entry));
+    DLSM_CHECK(ctx->tab.ensure(tabw));
+    DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p,
+                                   ctx->entries.p, ctx->tab.p, lgR, mode, s));
+    DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, slice, ctx->state.p, ctx->entries.p,
+                                ctx->tab.p, lgR, s));
+  } else {
+    DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, mode, s));
+    DLSM_TRY(launch_full_zero(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, s));
+    DLSM_TRY(launch_full_scatter(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, mode, s));
+  }
+  return DLSM_OK;
+}
+
+namespace {
+
+// Stage host keysets into one device buffer; returns per-job device keysets.
+// Variable-length sets are copied from offsets[0] and their offsets rebased.
+int stage_keys(dlsm_ctx* ctx, const dlsm_keyset* const* sets, int n, std::vector<dlsm_keyset>& dev) {
+  hipStream_t s = ctx->stream;
+  uint64_t bytes = 0, offs = 0;
+  std::vector<uint64_t> bpos(n), opos(n), src0(n), nb(n);
+  for (int j = 0; j < n; j++) {
+    const dlsm_keyset& k = *sets[j];
+    src0[j] = (k.offsets && k.n) ? k.offsets[0] : 0;
+    nb[j] = k.n == 0 ? 0 : (k.offsets ? k.offsets[k.n] - k.offsets[0] : k.n * uint64_t(k.key_len));
+    bpos[j] = bytes;
+    bytes += (nb[j] + 15) & ~uint64_t(15);
+    opos[j] = offs;
+    if (k.offsets) offs += k.n + 1;
+  }
+  DLSM_CHECK(ctx->st_keys.ensure(bytes + 16));
+  DLSM_CHECK(ctx->st_offs.ensure(offs + 1));
+  dev.resize(n);
+  for (int j = 0; j < n; j++) {
+    const dlsm_keyset& k = *sets[j];
+    dlsm_keyset d = k;
+    d.bytes = ctx->st_keys.p + bpos[j];
+    if (nb[j])
+      DLSM_TRY(hipMemcpyAsync(const_cast<uint8_t*>(d.bytes), k.bytes + src0[j], nb[j],
+                              hipMemcpyHostToDevice, s));
+    if (k.offsets) {
+      std::vector<uint64_t> ro(k.n + 1);
+      for (uint64_t i = 0; i <= k.n; i++) ro[i] = k.offsets[i] - src0[j];
+      d.offsets = ctx->st_offs.p + opos[j];
+      // pageable-source copies are staged before the call returns, so `ro`
+      // may be released right after.
+      DLSM_TRY(hipMemcpyAsync(const_cast<uint64_t*>(d.offsets), ro.data(),
+                              sizeof(uint64_t) * (k.n + 1), hipMemcpyHostToDevice, s));
+    }
+    dev[j] = d;
+  }
+  return DLSM_OK;
+}
+
+}  // namespace
+
+int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                          uint64_t* out_len) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  std::vector<const dlsm_keyset*> sets(n_jobs);
+  for (int j = 0; j < n_jobs; j++) {
+    DLSM_CHECK(validate_keyset(jobs[j].keys));
+    if (!jobs[j].out) return DLSM_E_ARG;
+    sets[j] = &jobs[j].keys;
+  }
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets.data(), n_jobs, dk));
+  std::vector<dlsm_build_job> dj(n_jobs);
+  uint64_t obytes = 0;
+  std::vector<uint64_t> opos(n_jobs);
+  for (int j = 0; j < n_jobs; j++) {
+    const uint64_t spec = full_filter_len(jobs[j].keys.n, bits_per_key);
+    const uint64_t cap = std::min(spec, jobs[j].out_cap);
+    opos[j] = obytes;
+    obytes += (cap + 255) & ~uint64_t(255);
+    dj[j].keys = dk[j];
+    dj[j].out_cap = cap;
+  }
+  DLSM_CHECK(ctx->st_out.ensure(obytes + 256));
+  DLSM_CHECK(ctx->st_len.ensure(n_jobs));
+  for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
+  DLSM_CHECK(dlsm_bloom_full_build_dev(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p));
+  hipStream_t s = ctx->stream;
+  DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
+  DLSM_TRY(hipStreamSynchronize(s));
+  int st = DLSM_OK;
+  for (int j = 0; j < n_jobs; j++) {
+    if (out_len[j] == 0) {
+      st = DLSM_E_CAPACITY;
+      continue;
+    }
+    DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
+  }
+  DLSM_TRY(hipStreamSynchronize(s));
+  return st;
+}
+
+// ---------------------------------------------------------------------------
+// Full filter probe
+// ---------------------------------------------------------------------------
+int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const uint64_t* lens,
+                          int n_filters, int filters_are_device, dlsm_filterset** out) {
+  if (!ctx || !out || !filters || !lens || n_filters < 1 || n_filters > 64) return DLSM_E_ARG;
+  *out = nullptr;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  // Metadata (k, num_lines) from each filter's 5-byte tail.
+  std::vector<FilterDev> h(n_filters);
+  std::vector<uint64_t> off(n_filters);
+  uint64_t blob = 0;
+  for (int f = 0; f < n_filters; f++) {
+    if (!filters[f] || lens[f] < 5) return DLSM_E_CORRUPT;
+    uint8_t tail[5];
+    const uint8_t* tp = filters[f] + lens[f] - 5;
+    if (filters_are_device) {
+      DLSM_TRY(hipMemcpyAsync(tail, tp, 5, hipMemcpyDeviceToHost, s));
+      DLSM_TRY(hipStreamSynchronize(s));
+    } else {
+      memcpy(tail, tp, 5);
+    }
+    int k, lg;
+    uint32_t L;
+    DLSM_CHECK(parse_tail(tail, lens[f], &k, &L, &lg));
+    h[f].L = L;
+    h[f].magic = fastmod_magic(L);
+    h[f].k = k;
+    h[f].lg = lg;
+    off[f] = blob;
+    blob += (lens[f] + 255) & ~uint64_t(255);
+  }
+  dlsm_filterset* fs = new (std::nothrow) dlsm_filterset();
+  if (!fs) return DLSM_E_NOMEM;
+  fs->device = ctx->device;
+  fs->F = n_filters;
+  fs->blob_bytes = blob;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&fs->blob), blob);
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&fs->d_filters), sizeof(FilterDev) * n_filters);
+  if (e != hipSuccess) {
+    dlsm_filterset_destroy(fs);
+    return from_hip(e);
+  }
+  for (int f = 0; f < n_filters; f++) {
+    e = hipMemcpyAsync(fs->blob + off[f], filters[f], lens[f],
+                       filters_are_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) break;
+    h[f].data = fs->blob + off[f];
+  }
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(fs->d_filters, h.data(), sizeof(FilterDev) * n_filters, hipMemcpyHostToDevice, s);
+  fs->h = h;
+  // Stackable: <= 8 filters, common line count and probe count, 64-byte lines.
+  bool stack = n_filters <= 8;
+  for (int f = 0; f < n_filters && stack; f++)
+    stack = h[f].lg == 6 && h[f].L == h[0].L && h[f].k == h[0].k;
+  if (e == hipSuccess && stack) {
+    fs->L = h[0].L;
+    fs->magic = h[0].magic;
+    fs->k = h[0].k;
+    e = hipMalloc(reinterpret_cast<void**>(&fs->stacked), static_cast<uint64_t>(fs->L) * 512u);
+    if (e == hipSuccess) e = launch_stack_filters(fs->d_filters, n_filters, fs->L, fs->stacked, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    dlsm_filterset_destroy(fs);
+    return from_hip(e);
+  }
+  *out = fs;
+  return DLSM_OK;
+}
+
+int dlsm_filterset_destroy(dlsm_filterset* fs) {
+  if (!fs) return DLSM_OK;
+  DeviceGuard g(fs->device);
+  if (fs->stacked) (void)hipFree(fs->stacked);
+  if (fs->d_filters) (void)hipFree(fs->d_filters);
+  if (fs->blob) (void)hipFree(fs->blob);
+  delete fs;
+  return DLSM_OK;
+}
+
+int dlsm_filterset_size(const dlsm_filterset* fs, int* n_filters, uint64_t* device_bytes) {
+  if (!fs) return DLSM_E_ARG;
+  if (n_filters) *n_filters = fs->F;
+  if (device_bytes)
+    *device_bytes = fs->blob_bytes + (fs->stacked ? static_cast<uint64_t>(fs->L) * 512u : 0);
+  return DLSM_OK;
+}
+
+int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
+                              uint8_t* mask_dev) {
+  if (!ctx || !fs || !keys) return DLSM_E_ARG;
+  if (fs->device != ctx->device) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!mask_dev) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  const int mode = is_k20(*keys) ? KM_K20 : KM_GENERIC;
+  const KeyDesc kd = to_desc(*keys);
+  const uint32_t S = fs->stacked ? ceil_div_u32(fs->L, kProbeSliceLines) : 0;
+  const bool sliced = ctx->path != 1 && fs->stacked && S >= 1 && S <= kMaxSlices &&
+                      keys->n <= 0xffffffffull * kProbeChunk;
+  if (ctx->path == 2 && !sliced) return DLSM_E_ARG;
+  if (!sliced) {
+    DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
+    return DLSM_OK;
+  }
+  const uint64_t n = keys->n;
+  const uint32_t nC = ceil_div_u32(n, kProbeChunk);
+  DLSM_CHECK(ctx->entries.ensure(n));
+  DLSM_CHECK(ctx->pos.ensure(n));
+  DLSM_CHECK(ctx->smask.ensure(n));
+  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(S + 1) * nC));
+  // Enough (slice, part) workgroups to fill 256 CUs several times over, and no
+  // part smaller than one chunk group.
+  int parts = static_cast<int>(std::max<uint32_t>(1, 2048u / S));
+  parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 64)));
+  const int lgR = 7;  // kProbeSliceLines
+  DLSM_TRY(launch_probe_partition(kd, fs->L, fs->magic, lgR, S, ctx->entries.p, ctx->pos.p,
+                                  ctx->tab.p, mode, s));
+  DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, n, ctx->entries.p,
+                               ctx->tab.p, ctx->smask.p, parts, s));
+  DLSM_TRY(launch_probe_unpermute(n, ctx->pos.p, ctx->smask.p, mask_dev, s));
+  return DLSM_OK;
+}
+
+int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
+                          uint8_t* mask) {
+  if (!ctx || !fs || !keys) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!mask) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  const dlsm_keyset* sets[1] = {keys};
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets, 1, dk));
+  const uint64_t mb = static_cast<uint64_t>((fs->F + 7) / 8) * keys->n;
+  DLSM_CHECK(ctx->st_out.ensure(mb));
+  DLSM_CHECK(dlsm_bloom_full_probe_dev(ctx, fs, &dk[0], ctx->st_out.p));
+  DLSM_TRY(hipMemcpyAsync(mask, ctx->st_out.p, mb, hipMemcpyDeviceToHost, ctx->stream));
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  return DLSM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Legacy FilterPolicy format (util/bloom.cc)
+// ---------------------------------------------------------------------------
+int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                int bits_per_key, uint64_t* out_len_dev) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  const int k = legacy_num_probes(bits_per_key);
+  bool all_k20 = true;
+  uint64_t ws = 0, total = 0;
+  std::vector<uint64_t> wpos(n_jobs), lens(n_jobs);
+  for (int j = 0; j < n_jobs; j++) {
+    DLSM_CHECK(validate_keyset(jobs[j].keys));
+    if (!jobs[j].out) return DLSM_E_ARG;
+    const uint64_t bits = legacy_bits(jobs[j].keys.n, bits_per_key);
+    lens[j] = bits / 8 + 1;
+    if (lens[j] > jobs[j].out_cap) return DLSM_E_CAPACITY;
+    wpos[j] = ws;
+    ws += (bits / 8 + 3 + 255) & ~uint64_t(255);
+    all_k20 = all_k20 && is_k20(jobs[j].keys);
+  }
+  const int mode = all_k20 ? KM_K20 : KM_GENERIC;
+  // Build into an aligned workspace (word atomics), then copy to the slots.
+  DLSM_CHECK(ctx->st_filter.ensure(ws + 256));
+  DLSM_TRY(hipMemsetAsync(ctx->st_filter.p, 0, ws, s));
+  for (int j0 = 0; j0 < n_jobs; j0 += 256) {
+    const int nj = std::min(256, n_jobs - j0);
+    std::vector<LegacyJobDev> hj(nj);
+    std::vector<uint64_t> key0s(nj);
+    uint64_t tk = 0;
+    for (int q = 0; q < nj; q++) {
+      const dlsm_build_job& b = jobs[j0 + q];
+      LegacyJobDev& d = hj[q];
+      d.keys = to_desc(b.keys);
+      d.out = ctx->st_filter.p + wpos[j0 + q];
+      d.bits = legacy_bits(b.keys.n, bits_per_key);
+      d.magic = d.bits <= 0xffffffffull ? fastmod_magic(static_cast<uint32_t>(d.bits)) : 0;
+      d.k = k;
+      d.key0 = tk;
+      key0s[q] = tk;
+      tk += b.keys.n;
+    }
+    total += tk;
+    DLSM_CHECK(ctx->ljobs.ensure(nj));
+    DLSM_CHECK(ctx->lstarts.ensure(nj));
+    DLSM_TRY(hipMemcpyAsync(ctx->ljobs.p, hj.data(), sizeof(LegacyJobDev) * nj, hipMemcpyHostToDevice, s));
+    DLSM_TRY(hipMemcpyAsync(ctx->lstarts.p, key0s.data(), sizeof(uint64_t) * nj, hipMemcpyHostToDevice, s));
+    DLSM_TRY(launch_legacy_scatter(ctx->ljobs.p, ctx->lstarts.p, nj, tk, mode, s));
+    // the job table is reused by the next group: keep the stream ordered
+  }
+  for (int j = 0; j < n_jobs; j++) {
+    DLSM_TRY(hipMemcpyAsync(jobs[j].out, ctx->st_filter.p + wpos[j], lens[j] - 1,
+                            hipMemcpyDeviceToDevice, s));
+    DLSM_TRY(hipMemsetAsync(jobs[j].out + lens[j] - 1, static_cast<int>(static_cast<uint8_t>(k)), 1, s));
+  }
+  DLSM_TRY(hipMemcpyAsync(out_len_dev, lens.data(), sizeof(uint64_t) * n_jobs, hipMemcpyHostToDevice, s));
+  (void)total;
+  return DLSM_OK;
+}
+
+int dlsm_bloom_legacy_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                            uint64_t* out_len) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  std::vector<const dlsm_keyset*> sets(n_jobs);
+  for (int j = 0; j < n_jobs; j++) {
+    DLSM_CHECK(validate_keyset(jobs[j].keys));
+    if (!jobs[j].out) return DLSM_E_ARG;
+    const uint64_t len = legacy_bits(jobs[j].keys.n, bits_per_key) / 8 + 1;
+    if (len > jobs[j].out_cap) return DLSM_E_CAPACITY;
+    sets[j] = &jobs[j].keys;
+  }
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets.data(), n_jobs, dk));
+  std::vector<dlsm_build_job> dj(n_jobs);
+  std::vector<uint64_t> opos(n_jobs);
+  uint64_t ob = 0;
+  for (int j = 0; j < n_jobs; j++) {
+    const uint64_t len = legacy_bits(jobs[j].keys.n, bits_per_key) / 8 + 1;
+    opos[j] = ob;
+    ob += (len + 255) & ~uint64_t(255);
+    dj[j].keys = dk[j];
+    dj[j].out_cap = len;
+  }
+  DLSM_CHECK(ctx->st_out.ensure(ob + 256));
+  DLSM_CHECK(ctx->st_len.ensure(n_jobs));
+  for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
+  DLSM_CHECK(dlsm_bloom_legacy_build_dev(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p));
+  hipStream_t s = ctx->stream;
+  for (int j = 0; j < n_jobs; j++) {
+    out_len[j] = dj[j].out_cap;
+    DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
+  }
+  DLSM_TRY(hipStreamSynchronize(s));
+  return DLSM_OK;
+}
+
+int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64_t len,
+                                const dlsm_keyset* keys, uint8_t* out_dev) {
+  if (!ctx || !keys) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!out_dev) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  // util/bloom.cc:57-81: len < 2 -> false; k (signed char -> size_t) > 30 -> true.
+  int trivial = 0, k = 0;
+  uint64_t bits = 0;
+  if (len < 2 || !filter_dev) {
+    trivial = 1;
+  } else {
+    uint8_t kb;
+    DLSM_TRY(hipMemcpyAsync(&kb, filter_dev + len - 1, 1, hipMemcpyDeviceToHost, s));
+    DLSM_TRY(hipStreamSynchronize(s));
+    const int ks = static_cast<int>(static_cast<int8_t>(kb));
+    if (ks < 0 || ks > 30) trivial = 2;
+    else if (ks == 0) trivial = 2;  // zero probes -> match
+    k = ks;
+    bits = (len - 1) * 8;
+  }
+  const uint32_t magic = (bits && bits <= 0xffffffffull) ? fastmod_magic(static_cast<uint32_t>(bits)) : 0;
+  const int mode = is_k20(*keys) ? KM_K20 : KM_GENERIC;
+  DLSM_TRY(launch_legacy_probe(filter_dev, bits, magic, k, trivial, to_desc(*keys), out_dev, mode, s));
+  return DLSM_OK;
+}
+
+int dlsm_bloom_legacy_probe(dlsm_ctx* ctx, const uint8_t* filter, uint64_t len,
+                            const dlsm_keyset* keys, uint8_t* out) {
+  if (!ctx || !keys) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!out) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  const dlsm_keyset* sets[1] = {keys};
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets, 1, dk));
+  const uint8_t* fdev = nullptr;
+  if (filter && len) {
+    DLSM_CHECK(ctx->st_filter.ensure(len));
+    DLSM_TRY(hipMemcpyAsync(ctx->st_filter.p, filter, len, hipMemcpyHostToDevice, s));
+    fdev = ctx->st_filter.p;
+  }
+  DLSM_CHECK(ctx->st_out.ensure(keys->n));
+  DLSM_CHECK(dlsm_bloom_legacy_probe_dev(ctx, fdev, len, &dk[0], ctx->st_out.p));
+  DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p, keys->n, hipMemcpyDeviceToHost, s));
+  DLSM_TRY(hipStreamSynchronize(s));
+  return DLSM_OK;
+}
+
+}  // extern "C"

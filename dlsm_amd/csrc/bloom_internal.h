@@ -1,0 +1,104 @@
+// dlsm_amd/csrc/bloom_internal.h -- device-side descriptors and the launcher
+// interface between the C ABI (bloom_capi.hip) and the kernels
+// (bloom_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bloom_math.h"
+
+namespace dlsm {
+
+// Key-load modes: K20 = fixed 20-byte keys at a 4-byte-aligned base (the
+// BASELINE shape), GENERIC = any fixed length / alignment or offsets.
+enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1 };
+
+struct KeyDesc {
+  const uint8_t* bytes;
+  const uint64_t* offsets;  // n+1 entries or nullptr
+  uint64_t n;
+  uint32_t key_len;
+  uint32_t pad;
+};
+
+// One full-filter build job as the kernels see it.
+struct FullJobDev {
+  KeyDesc keys;
+  uint8_t* out;
+  uint64_t out_cap;
+  uint64_t* out_len;   // device slot for this job's length
+  uint64_t entry0;     // first entry of this job in the entry workspace
+  uint64_t tab0;       // first word of this job's (n_slices+1) x n_chunks table
+  uint32_t chunk0, n_chunks;
+  uint32_t slice0, n_slices;
+  uint32_t L_spec, magic_spec;  // speculative line count (no duplicates) + fastmod magic
+  int32_t k, bpk;
+};
+
+// Per-job device state written by the partition/count kernels.
+struct JobState {
+  unsigned long long distinct;  // consecutive-distinct hash count (AddKey dedup)
+  int32_t status;
+  uint32_t pad;
+};
+
+// A parsed full filter resident on the device (FullFilterBlockReader state).
+struct FilterDev {
+  const uint8_t* data;
+  uint32_t L, magic;
+  int32_t k, lg;
+};
+
+// Legacy-format build job.
+struct LegacyJobDev {
+  KeyDesc keys;
+  uint8_t* out;
+  uint64_t bits;      // filter bits (multiple of 8)
+  uint32_t magic;     // fastmod magic for bits when bits < 2^32
+  int32_t k;
+  uint64_t key0;      // global index of this job's first key (flattened grid)
+};
+
+constexpr int kBlock = 256;
+constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
+constexpr int kBuildChunk = 4096;   // keys per partition chunk (build)
+constexpr int kProbeChunk = 8192;   // keys per partition chunk (probe)
+constexpr int kProbeSliceLines = 128;  // 128 lines x 512 B stacked = 64 KiB LDS
+
+// ---- launchers (bloom_kernels.hip) -----------------------------------------
+// All return hipError_t of the launch.
+hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                             uint32_t total_chunks, JobState* st, int mode, hipStream_t s);
+hipError_t launch_full_finalize(const FullJobDev* jobs, int n_jobs, JobState* st, hipStream_t s);
+hipError_t launch_full_zero(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                            uint32_t total_chunks, JobState* st, hipStream_t s);
+hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                               uint32_t total_chunks, JobState* st, int mode, hipStream_t s);
+
+hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                                 uint32_t total_chunks, JobState* st, uint32_t* entries,
+                                 uint32_t* tab, int lgR, int mode, hipStream_t s);
+hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
+                              uint32_t total_slices, JobState* st, const uint32_t* entries,
+                              const uint32_t* tab, int lgR, hipStream_t s);
+
+hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
+                               int mode, hipStream_t s);
+hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, uint64_t* stacked,
+                                hipStream_t s);
+hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
+                                  uint32_t n_slices, uint32_t* entries, uint16_t* pos,
+                                  uint32_t* tab, int mode, hipStream_t s);
+hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
+                               int lgR, uint32_t n_slices, uint32_t n_chunks, uint64_t n_keys,
+                               const uint32_t* entries, const uint32_t* tab, uint8_t* smask,
+                               int parts, hipStream_t s);
+hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
+                                  uint8_t* mask, hipStream_t s);
+
+hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s, int n_jobs,
+                                 uint64_t total_keys, int mode, hipStream_t s);
+hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,
+                               int trivial, KeyDesc keys, uint8_t* out, int mode, hipStream_t s);
+
+}  // namespace dlsm

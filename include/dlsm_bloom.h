@@ -1,0 +1,178 @@
+/*
+ * dlsm_bloom.h -- C ABI of the MI355X-native SSTable Bloom-filter engine.
+ *
+ * Drop-in boundary for dLSM's (TimberSaw) filter hot path.  Plain C types
+ * only: pointers, sizes, status codes.  No exceptions cross this boundary
+ * (the reference builds with -fno-exceptions, CMakeLists.txt:79-81).
+ *
+ * Reference interfaces replaced (file:line in ruihong123/dLSM):
+ *   BloomHash                      include/TimberSaw/filter_policy.h:26-28
+ *   FullFilterBlockBuilder         table/full_filter_block.h:33-70,
+ *       AddKey/Finish              table/full_filter_block.cc:39-141
+ *   FullFilterBlockReader          table/full_filter_block.h:71-94,
+ *       ctor / KeyMayMatch         table/full_filter_block.cc:186-284
+ *   FilterPolicy / BloomFilterPolicy include/TimberSaw/filter_policy.h:31-71,
+ *       CreateFilter/KeyMayMatch   util/bloom.cc:25-81
+ * See INTEGRATION.md for the reference-side binding.
+ *
+ * Output format: byte-identical to the reference on the same inputs.  The
+ * reference ORs bits into caller-zeroed RDMA slots (full_filter_block.cc:99-108
+ * after table_builder_computeside.cc:38,48); this library writes every byte of
+ * the filter (zeros included), so the result equals the reference's on a
+ * zeroed slot, which every reference caller guarantees.
+ *
+ * Memory: functions suffixed _dev take DEVICE pointers (keys, offsets, output
+ * slots, masks) and are asynchronous on the context's stream.  Unsuffixed
+ * functions take HOST pointers, stage through device memory, and return after
+ * the result is in the host buffer (the reference's synchronous call shape).
+ */
+#ifndef DLSM_BLOOM_H_
+#define DLSM_BLOOM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DLSM_BLOOM_ABI_VERSION 1
+
+/* Status codes (full_filter_block.cc:192-249 exit(1)s become DLSM_E_CORRUPT). */
+#define DLSM_OK 0
+#define DLSM_E_ARG (-1)      /* bad argument / unsupported shape */
+#define DLSM_E_CAPACITY (-2) /* output slot too small (the reference only asserts, :103) */
+#define DLSM_E_CORRUPT (-3)  /* filter metadata the reference rejects or cannot probe */
+#define DLSM_E_DEVICE (-4)   /* HIP runtime error */
+#define DLSM_E_NOMEM (-5)    /* device allocation failed */
+
+typedef struct dlsm_ctx dlsm_ctx;             /* one device + one stream + workspace */
+typedef struct dlsm_filterset dlsm_filterset; /* F parsed full filters resident on a device */
+
+/* A packed key set.  Fixed-length keys: offsets == NULL and every key is
+ * key_len bytes at bytes + i*key_len.  Variable-length keys: offsets has n+1
+ * entries and key i is bytes[offsets[i], offsets[i+1]).  The reference hashes
+ * user keys (ExtractUserKey, db/dbformat.h:374-377): callers strip the 8-byte
+ * internal-key trailer before handing keys over, exactly as
+ * table_builder_computeside.cc:222-224 does. */
+typedef struct {
+  const uint8_t* bytes;
+  const uint64_t* offsets;
+  uint32_t key_len;
+  uint32_t reserved;
+  uint64_t n;
+} dlsm_keyset;
+
+/* One SSTable's filter: its keys in table order and its output slot. */
+typedef struct {
+  dlsm_keyset keys;
+  uint8_t* out;     /* output slot (4-byte aligned) */
+  uint64_t out_cap; /* slot capacity in bytes */
+} dlsm_build_job;
+
+/* ---- host-only helpers (no device touched) ------------------------------ */
+
+const char* dlsm_strerror(int status);
+int dlsm_abi_version(void);
+
+/* BloomHash(key) = Hash(key, n, 0xbc9f1d34); util/hash.cc:22-62 and
+ * include/TimberSaw/filter_policy.h:26-28 (tail bytes sign-extended). */
+uint32_t dlsm_bloom_hash(const void* key, size_t n);
+
+/* ChooseNumProbes: util/bloom_impl.h:351-357 (full filter, via
+ * full_filter_block.cc:19). */
+int dlsm_bloom_full_num_probes(int bits_per_key);
+
+/* CalculateSpace for n_dedup consecutive-distinct hashes:
+ * table/full_filter_block.cc:61-92.  nbytes = num_lines*64 + 5. */
+int dlsm_bloom_full_size(uint64_t n_dedup, int bits_per_key, uint32_t* num_lines,
+                         uint64_t* nbytes);
+
+/* BloomFilterPolicy::CreateFilter output size (bytes + the k byte):
+ * util/bloom.cc:27-34,53-54. */
+int dlsm_bloom_legacy_size(uint64_t n, int bits_per_key, uint64_t* nbytes);
+
+/* FullFilterBlockReader ctor metadata parse: table/full_filter_block.cc:186-252.
+ * Returns DLSM_E_CORRUPT where the reference exit(1)s, and also for filters the
+ * reference accepts but cannot probe without undefined behaviour (<= 5 bytes:
+ * h % 0).  log2_line is 6 in the common case and 0 in the reference's
+ * "len % num_lines == 0" branch (log2_cache_line_size_ left at 0). */
+int dlsm_bloom_full_parse(const uint8_t* filter, uint64_t len, int* num_probes,
+                          uint32_t* num_lines, int* log2_line);
+
+/* ---- context ------------------------------------------------------------ */
+
+int dlsm_device_count(int* n);
+int dlsm_ctx_create(int device, dlsm_ctx** out);
+int dlsm_ctx_destroy(dlsm_ctx* ctx);
+/* Work on the caller's hipStream_t (e.g. torch.cuda.current_stream()); NULL
+ * restores the context's own stream. */
+int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
+void* dlsm_ctx_stream(dlsm_ctx* ctx);
+int dlsm_ctx_sync(dlsm_ctx* ctx);
+/* Pre-size the device workspace so later calls never allocate (graph capture). */
+int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs);
+/* Select kernels: 0 = auto, 1 = direct (global atomics / global probes),
+ * 2 = sliced (LDS-tiled).  For A/B measurement; results are identical. */
+int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
+
+/* Page-lock a host range (e.g. an RDMA-registered FilterChunk slot) so D2H
+ * copies land in it directly. */
+int dlsm_host_register(void* p, size_t len);
+int dlsm_host_unregister(void* p);
+
+/* ---- full filter (SSTable format), build -------------------------------- */
+
+/* Build one full filter per job: FullFilterBlockBuilder(mr, bpk); AddKey(k)
+ * for every key in order; Finish().  Device pointers; asynchronous.
+ * out_len_dev: device uint64[n_jobs] receiving each filter's length
+ * (num_lines*64+5), or 0 when that job's slot was too small. */
+int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                              int bits_per_key, uint64_t* out_len_dev);
+
+/* Same with host keys and host output slots (H2D + build + D2H, synchronous).
+ * out_len: host uint64[n_jobs].  Returns DLSM_E_CAPACITY if any slot is too
+ * small (its out_len is 0). */
+int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                          int bits_per_key, uint64_t* out_len);
+
+/* ---- full filter, probe ------------------------------------------------- */
+
+/* Parse + upload F full filters (1 <= F <= 64), FullFilterBlockReader ctor
+ * semantics for each.  filters_are_device: the filter pointers are device
+ * pointers already resident on ctx's device.  The set keeps its own copy. */
+int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const uint64_t* lens,
+                          int n_filters, int filters_are_device, dlsm_filterset** out);
+int dlsm_filterset_destroy(dlsm_filterset* fs);
+int dlsm_filterset_size(const dlsm_filterset* fs, int* n_filters, uint64_t* device_bytes);
+
+/* KeyMayMatch of every key against every filter of the set.  mask has
+ * n * ceil(F/8) bytes; bit f of key i's bytes = filter f's answer.  Device
+ * pointers; asynchronous. */
+int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
+                              uint8_t* mask_dev);
+/* Host keys and host mask, synchronous. */
+int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
+                          uint8_t* mask);
+
+/* ---- legacy FilterPolicy format (util/bloom.cc) ------------------------- */
+
+/* CreateFilter(keys, n, dst) per job: writes bytes+1 bytes at out.
+ * out_len_dev: device uint64[n_jobs]. */
+int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                int bits_per_key, uint64_t* out_len_dev);
+int dlsm_bloom_legacy_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                            int bits_per_key, uint64_t* out_len);
+
+/* KeyMayMatch(key, filter) for every key against one legacy filter; out has one
+ * byte (0/1) per key.  filter is a device (``_dev``) or host pointer. */
+int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64_t len,
+                                const dlsm_keyset* keys, uint8_t* out_dev);
+int dlsm_bloom_legacy_probe(dlsm_ctx* ctx, const uint8_t* filter, uint64_t len,
+                            const dlsm_keyset* keys, uint8_t* out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* DLSM_BLOOM_H_ */

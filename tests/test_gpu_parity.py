@@ -1,0 +1,392 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the
+reference-generated golden fixtures.  Bit-exact for every byte and every
+probe answer; both kernel families (direct, sliced) are checked."""
+import numpy as np
+import pytest
+
+from tests._util import case_keys
+
+pytestmark = pytest.mark.gpu
+
+PATHS = [0, 1, 2]  # auto, direct, sliced
+
+
+def keys_of(case):
+    import dlsm_amd
+
+    data, offs, stride, n = case_keys(case)
+    if offs is None:
+        return dlsm_amd.Keys(data, n, stride, None)
+    return dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]), n, 0, offs)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_build_golden_cases(gpu, golden, path):
+    gpu.set_path(path)
+    try:
+        for c in golden["full"]["cases"]:
+            got = gpu.full_build([keys_of(c)], c["bpk"])[0]
+            assert got.hex() == c["filter"], (c["name"], path)
+    finally:
+        gpu.set_path(0)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_build_golden_batch(gpu, golden, path):
+    """All golden cases with bpk 10 as ONE batched call (mixed shapes -> generic keys)."""
+    cases = [c for c in golden["full"]["cases"] if c["bpk"] == 10]
+    gpu.set_path(path)
+    try:
+        got = gpu.full_build([keys_of(c) for c in cases], 10)
+    finally:
+        gpu.set_path(0)
+    for c, g in zip(cases, got):
+        assert g.hex() == c["filter"], c["name"]
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_build_digests(gpu, golden, orc, path):
+    import dlsm_amd
+
+    gpu.set_path(path)
+    try:
+        for d in golden["full"]["digests"]:
+            if d.get("format") == "legacy":
+                continue
+            keys = orc.dbbench_keys(d["first"], d["step"], d["n"])
+            f = gpu.full_build([dlsm_amd.Keys(keys, d["n"], 20)], d["bpk"])[0]
+            assert len(f) == d["len"] and orc.fnv1a64(f) == d["fnv1a64"], (d["name"], path)
+    finally:
+        gpu.set_path(0)
+
+
+def test_full_build_dev_config4_batch(gpu, orc):
+    """16 SSTables (12 subcompaction + 4 flush) in one device-resident call."""
+    import torch
+
+    import dlsm_amd
+
+    n = 153_846
+    tables, outs, want = [], [], []
+    for s in range(16):
+        k = orc.dbbench_keys(s, 16, n)
+        want.append(orc.full_build(k, n))
+        tables.append(dlsm_amd.Keys(torch.from_numpy(k).cuda(), n, 20))
+        outs.append(torch.zeros(dlsm_amd.full_size(n)[0] + 64, dtype=torch.uint8, device="cuda"))
+    lens = torch.zeros(16, dtype=torch.uint64, device="cuda")
+    for path in (1, 2):
+        for o in outs:
+            o.fill_(0xEE)  # garbage: the library must write every filter byte
+        gpu.set_path(path)
+        gpu.full_build_dev(tables, outs, lens, 10)
+        gpu.sync()
+        gpu.set_path(0)
+        L = lens.cpu().numpy()
+        for s in range(16):
+            assert int(L[s]) == len(want[s])
+            got = outs[s][: int(L[s])].cpu().numpy().tobytes()
+            assert got == want[s], (s, path)
+            assert (outs[s][int(L[s]):].cpu().numpy() == 0xEE).all()  # nothing past the filter
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_build_random_varlen_and_unaligned(gpu, orc, path):
+    import dlsm_amd
+
+    rng = np.random.default_rng(99)
+    tables, want = [], []
+    for t in range(12):
+        n = int(rng.choice([0, 1, 2, 3, 50, 51, 52, 4095, 4096, 4097, 9000, 20000]))
+        keys = [bytes(rng.integers(0, 256, int(rng.integers(0, 45)), dtype=np.uint8)) for _ in range(n)]
+        # inject adjacent duplicates and repeats
+        if n > 10:
+            for q in rng.integers(1, n, 5):
+                keys[int(q)] = keys[int(q) - 1]
+        data, offs = orc.pack_var(keys)
+        want.append(orc.full_build(data, n, stride=0, offsets=offs))
+        pad = np.concatenate([np.zeros(3, np.uint8), data, np.zeros(16, np.uint8)])
+        tables.append(dlsm_amd.Keys(pad, n, 0, offs + 3))  # unaligned start via offsets
+    gpu.set_path(path)
+    try:
+        got = gpu.full_build(tables, 10)
+    finally:
+        gpu.set_path(0)
+    for t in range(len(want)):
+        assert got[t] == want[t], (t, path)
+
+
+@pytest.mark.parametrize("path", [1, 2])
+def test_full_build_fixed_nonaligned_lengths(gpu, orc, path):
+    import dlsm_amd
+
+    for klen in (1, 3, 7, 8, 16, 21, 24, 29):
+        n = 7000
+        raw = np.random.default_rng(klen).integers(0, 256, n * klen + 16, dtype=np.uint8)
+        want = orc.full_build(raw, n, stride=klen)
+        gpu.set_path(path)
+        try:
+            got = gpu.full_build([dlsm_amd.Keys(raw, n, klen)], 10)[0]
+        finally:
+            gpu.set_path(0)
+        assert got == want, (klen, path)
+
+
+def test_full_build_dedup_changes_line_count_large(gpu, orc):
+    """Enough adjacent duplicates to lower L below the speculative count, at a
+    size where the sliced path has many slices (slow-path re-scan)."""
+    import dlsm_amd
+
+    n = 300_000
+    v = np.arange(n, dtype=np.uint64)
+    v[1::3] = v[0::3][: v[1::3].size]  # every third key repeats its predecessor
+    keys = orc.keys_from_values(v)
+    want = orc.full_build(keys, n)
+    assert orc.full_dedup_count(keys, n) < n
+    assert len(want) < dlsm_amd.full_size(n)[0]
+    for path in (1, 2):
+        gpu.set_path(path)
+        got = gpu.full_build([dlsm_amd.Keys(keys, n, 20)], 10)[0]
+        gpu.set_path(0)
+        assert got == want, path
+
+
+def test_full_build_capacity_error(gpu, orc):
+    import dlsm_amd
+
+    keys = orc.dbbench_keys(0, 1, 1000)
+    need = dlsm_amd.full_size(1000)[0]
+    with pytest.raises(dlsm_amd.DlsmError) as e:
+        gpu.full_build([dlsm_amd.Keys(keys, 1000, 20)], 10, caps=[need - 1])
+    assert e.value.status == -2
+
+
+def test_full_build_bits_per_key_sweep(gpu, orc):
+    import dlsm_amd
+
+    keys = orc.dbbench_keys(17, 5, 5000)
+    for bpk in (0, 1, 2, 3, 7, 10, 15, 20, 33, 44, 64):
+        want = orc.full_build(keys, 5000, bpk=bpk)
+        for path in (1, 2):
+            gpu.set_path(path)
+            got = gpu.full_build([dlsm_amd.Keys(keys, 5000, 20)], bpk)[0]
+            gpu.set_path(0)
+            assert got == want, (bpk, path)
+
+
+# ---------------------------------------------------------------------------
+# probe
+# ---------------------------------------------------------------------------
+
+def test_full_probe_golden(gpu, golden, orc):
+    import dlsm_amd
+
+    g = golden["probe"]
+    filters = [bytes.fromhex(f["filter"]) for f in g["filters"]]
+    q = g["queries"]
+    keys = orc.dbbench_keys(q["first"], q["step"], q["n"])
+    fs = gpu.filterset(filters)
+    mask = gpu.full_probe(fs, dlsm_amd.Keys(keys, q["n"], 20))
+    for f, ans in enumerate(g["answers"]):
+        want = np.frombuffer(bytes.fromhex(ans), dtype=np.uint8)
+        assert np.array_equal((mask >> f) & 1, want), f
+
+
+@pytest.mark.parametrize("F", [1, 3, 8])
+def test_full_probe_stacked_vs_oracle(gpu, orc, F):
+    """Equal-L filter sets take the sliced (LDS) probe; compare with direct + oracle."""
+    import dlsm_amd
+
+    n_per = 200_000
+    filters = [orc.full_build(orc.dbbench_keys(f, 8, n_per), n_per) for f in range(F)]
+    nq = 700_001
+    vals = orc.mt_values(1000, 8 * n_per * 2, nq)
+    q = orc.keys_from_values(vals)
+    want = orc.full_probe(filters, q, nq, nthreads=8)
+    fs = gpu.filterset(filters)
+    for path in PATHS:
+        gpu.set_path(path)
+        got = gpu.full_probe(fs, dlsm_amd.Keys(q, nq, 20))
+        gpu.set_path(0)
+        assert np.array_equal(got, want), path
+    # keys that are in filter f must answer 1 for f
+    assert ((want & 1)[vals % 8 == 0][vals[vals % 8 == 0] < 8 * n_per] == 1).all()
+
+
+def test_full_probe_many_filters_and_varlen(gpu, orc):
+    import dlsm_amd
+
+    rng = np.random.default_rng(5)
+    filters = []
+    for f in range(13):  # > 8 -> 2 mask bytes, mixed L
+        n = int(rng.integers(1, 5000))
+        filters.append(orc.full_build(orc.dbbench_keys(int(rng.integers(0, 10000)), 1, n), n))
+    keys = [bytes(rng.integers(0, 256, int(rng.integers(0, 30)), dtype=np.uint8)) for _ in range(3000)]
+    keys += [orc.dbbench_keys(v, 1, 1).tobytes() for v in range(0, 12000, 7)]
+    data, offs = orc.pack_var(keys)
+    want = orc.full_probe(filters, data, len(keys), stride=0, offsets=offs)
+    fs = gpu.filterset(filters)
+    got = gpu.full_probe(fs, dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]),
+                                           len(keys), 0, offs))
+    assert np.array_equal(got, want)
+
+
+def test_full_probe_log2_zero_branch(gpu, orc):
+    """A filter whose num_lines*64 != len but len % num_lines == 0: the reference
+    probes it with log2_cache_line_size_ == 0 (full_filter_block.h:85)."""
+    import dlsm_amd
+
+    rng = np.random.default_rng(3)
+    body = rng.integers(0, 256, 96, dtype=np.uint8).tobytes()
+    filt = body + bytes([6, 3, 0, 0, 0])  # L = 3, len 96 = 3 * 32
+    st, k, L, lg = dlsm_amd.full_parse(filt)
+    assert st == 0 and lg == 0
+    q = orc.dbbench_keys(0, 1, 5000)
+    want = orc.full_probe([filt], q, 5000)
+    got = gpu.full_probe(gpu.filterset([filt]), dlsm_amd.Keys(q, 5000, 20))
+    assert np.array_equal(got, want)
+
+
+def test_full_probe_corrupt_filters(gpu):
+    import dlsm_amd
+
+    for bad in [b"", b"\x06", bytes([6, 0, 0, 0, 0]), bytes(64) + bytes([0, 1, 0, 0, 0]),
+                bytes(64) + bytes([0x80, 1, 0, 0, 0]), bytes(100) + bytes([6, 3, 0, 0, 0])]:
+        with pytest.raises(dlsm_amd.DlsmError) as e:
+            gpu.filterset([bad])
+        assert e.value.status == -3
+
+
+def test_full_probe_dev_torch(gpu, orc):
+    import torch
+
+    import dlsm_amd
+
+    filters = [orc.full_build(orc.dbbench_keys(f, 4, 50_000), 50_000) for f in range(4)]
+    nq = 123_457
+    q = orc.keys_from_values(orc.mt_values(7, 400_000, nq))
+    want = orc.full_probe(filters, q, nq)
+    fdev = [torch.from_numpy(np.frombuffer(f, np.uint8).copy()).cuda() for f in filters]
+    fs = gpu.filterset(fdev, on_device=True)
+    qd = torch.from_numpy(q).cuda()
+    mask = torch.zeros(nq, dtype=torch.uint8, device="cuda")
+    gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy(), want)
+
+
+# ---------------------------------------------------------------------------
+# legacy FilterPolicy format
+# ---------------------------------------------------------------------------
+
+def test_legacy_golden(gpu, golden, orc):
+    import dlsm_amd
+
+    g = golden["legacy"]
+    for c in g["cases"]:
+        got = gpu.legacy_build([keys_of(c)], c["bpk"])[0]
+        assert got.hex() == c["filter"], c["name"]
+    f = bytes.fromhex(g["small"]["filter"])
+    for q, want in g["small"]["queries"].items():
+        assert gpu.legacy_probe(f, dlsm_amd.Keys.pack([q.encode()]))[0] == want
+    for e in g["edges"]:
+        fb = bytes.fromhex(e["filter"])
+        keys = orc.dbbench_keys(e["query_first"], 1, len(e["answers"]))
+        got = gpu.legacy_probe(fb, dlsm_amd.Keys(keys, len(e["answers"]), 20))
+        assert list(got) == e["answers"], e.get("k_byte")
+
+
+def test_legacy_random_vs_oracle(gpu, orc):
+    import dlsm_amd
+
+    rng = np.random.default_rng(11)
+    tables, want = [], []
+    for n in (0, 1, 5, 6, 7, 64, 1000, 33333):
+        keys = [bytes(rng.integers(0, 256, int(rng.integers(0, 25)), dtype=np.uint8)) for _ in range(n)]
+        data, offs = orc.pack_var(keys)
+        want.append(orc.legacy_build(data, n, stride=0, offsets=offs))
+        tables.append(dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]), n, 0, offs))
+    got = gpu.legacy_build(tables, 10)
+    assert got == want
+    q = orc.dbbench_keys(0, 3, 20000)
+    for f in want:
+        assert np.array_equal(gpu.legacy_probe(f, dlsm_amd.Keys(q, 20000, 20)),
+                              orc.legacy_probe(f, q, 20000))
+
+
+def test_bloom_test_semantics_on_gpu(gpu):
+    """util/bloom_test.cc:82-150 (EmptyFilter, Small, VaryingLengths) on the GPU policy."""
+    import struct
+
+    import dlsm_amd
+
+    pol = dlsm_amd.BloomFilterPolicy(10, gpu)
+    assert pol.Name() == "TimberSaw.BuiltinBloomFilter2"
+    empty = bytearray()
+    pol.CreateFilter([], 0, empty)
+    assert not pol.KeyMayMatch(b"hello", bytes(empty))
+    small = bytearray()
+    pol.CreateFilter([b"hello", b"world"], 2, small)
+    assert pol.KeyMayMatch(b"hello", bytes(small)) and pol.KeyMayMatch(b"world", bytes(small))
+    assert not pol.KeyMayMatch(b"x", bytes(small)) and not pol.KeyMayMatch(b"foo", bytes(small))
+    good = mediocre = 0
+    length = 1
+    while length <= 10000:
+        keys = [struct.pack("<I", i) for i in range(length)]
+        f = bytearray()
+        pol.CreateFilter(keys, length, f)
+        assert len(f) <= length * 10 // 8 + 40
+        assert pol.KeysMayMatch(dlsm_amd.Keys.pack(keys), bytes(f)).all()
+        qk = dlsm_amd.Keys.pack([struct.pack("<I", i + 1000000000) for i in range(10000)])
+        rate = pol.KeysMayMatch(qk, bytes(f)).mean()
+        assert rate <= 0.02
+        good, mediocre = (good, mediocre + 1) if rate > 0.0125 else (good + 1, mediocre)
+        length = length + 1 if length < 10 else length + 10 if length < 100 else \
+            length + 100 if length < 1000 else length + 1000
+    assert mediocre <= good / 5
+
+
+# ---------------------------------------------------------------------------
+# reference-shaped classes and full-size properties
+# ---------------------------------------------------------------------------
+
+def test_full_filter_block_builder_and_reader(gpu, orc):
+    import dlsm_amd
+
+    slot = np.zeros(256 * 1024, dtype=np.uint8)  # FILTER_BLOCK slot (options.h:28)
+    b = dlsm_amd.FullFilterBlockBuilder(slot, 10, gpu)
+    b.RestartBlock(0)
+    keys = orc.dbbench_keys(0, 1, 20_000)
+    for i in range(20_000):
+        b.AddKey(keys[i * 20:(i + 1) * 20].tobytes())
+    b.Finish()
+    want = orc.full_build(keys, 20_000)
+    assert bytes(b.result) == want
+    r = dlsm_amd.FullFilterBlockReader(bytes(b.result), gpu)
+    assert r.num_probes_ == 6 and r.num_lines_ == dlsm_amd.full_size(20_000)[1]
+    assert r.KeyMayMatch(keys[:20].tobytes())
+    q = orc.dbbench_keys(0, 1, 40_000)
+    assert np.array_equal(r.KeysMayMatch(dlsm_amd.Keys(q, 40_000, 20)),
+                          orc.full_probe([want], q, 40_000).astype(bool))
+    b.Reset()
+    assert len(b.result) == 0
+
+
+def test_full_size_properties(gpu, orc):
+    """At BASELINE size (1.6M keys): no false negatives, FP ~1.2 %, probe of
+    a stacked set agrees with single-filter probes (size-independent checks)."""
+    import dlsm_amd
+
+    n = 1_600_000
+    tabs = [dlsm_amd.Keys(orc.dbbench_keys(f, 8, n), n, 20) for f in range(8)]
+    filters = gpu.full_build(tabs, 10)
+    fs = gpu.filterset(filters)
+    for f in range(8):
+        m = gpu.full_probe(fs, tabs[f])
+        assert ((m >> f) & 1).all(), f
+    absent = dlsm_amd.Keys(orc.dbbench_keys(8 * n + 12345, 1, 1_000_000), 1_000_000, 20)
+    m = gpu.full_probe(fs, absent)
+    fp = np.unpackbits(m[:, None], axis=1).mean()
+    assert 0.008 < fp < 0.016, fp
+    single = gpu.filterset([filters[3]])
+    m3 = gpu.full_probe(single, absent)
+    assert np.array_equal(m3 & 1, (m >> 3) & 1)
