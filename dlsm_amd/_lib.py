@@ -78,6 +78,15 @@ _LIB = None
 def _lib():
     global _LIB
     if _LIB is None:
+        # One HIP runtime per process: torch ships its own libamdhip64 (soname
+        # libamdhip64.so.7, but its users NEED the unversioned name).  Loading
+        # torch first makes our NEEDED libamdhip64.so.7 bind to that same copy;
+        # loading ours first would put two runtimes in the process and torch
+        # then sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(
                 f"dlsm_amd: HIP library not built ({LIB_PATH} missing); run `make` or "
