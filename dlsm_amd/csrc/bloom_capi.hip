@@ -78,7 +78,11 @@ struct dlsm_ctx {
   DevBuf<uint32_t> tab;
   DevBuf<FullJobDev> jobs;
   DevBuf<uint32_t> starts;  // chunk0s | slice0s
-  DevBuf<JobState> state;
+  DevBuf<uint32_t> dchunk;  // per-chunk consecutive-distinct counts
+  DevBuf<uint32_t> jobL;    // per-job line count (direct path)
+  // last uploaded job table (skip the H2D when a caller repeats a batch)
+  std::vector<FullJobDev> last_jobs;
+  std::vector<uint32_t> last_starts;
   DevBuf<LegacyJobDev> ljobs;
   DevBuf<uint64_t> lstarts;
   // probe workspace
@@ -138,8 +142,9 @@ KeyDesc to_desc(const dlsm_keyset& k) {
   return d;
 }
 
+// The K20 kernels stage keys through LDS with 16-byte loads.
 bool is_k20(const dlsm_keyset& k) {
-  return k.offsets == nullptr && k.key_len == 20 && (k.n == 0 || aligned(k.bytes, 4));
+  return k.offsets == nullptr && k.key_len == 20 && (k.n == 0 || aligned(k.bytes, 16));
 }
 
 // Slice width for the sliced build: the smallest 2^lgR (lgR in [9, 11]) that
@@ -265,7 +270,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->tab.release();
   ctx->jobs.release();
   ctx->starts.release();
-  ctx->state.release();
+  ctx->dchunk.release();
+  ctx->jobL.release();
   ctx->ljobs.release();
   ctx->lstarts.release();
   ctx->pos.release();
@@ -311,7 +317,8 @@ int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   DLSM_CHECK(ctx->tab.ensure(chunks * (kMaxSlices + 1)));
   DLSM_CHECK(ctx->jobs.ensure(max_jobs));
   DLSM_CHECK(ctx->starts.ensure(2 * (max_jobs + 1)));
-  DLSM_CHECK(ctx->state.ensure(max_jobs));
+  DLSM_CHECK(ctx->dchunk.ensure(chunks));
+  DLSM_CHECK(ctx->jobL.ensure(max_jobs));
   return DLSM_OK;
 }
 
@@ -380,27 +387,34 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     tabw += static_cast<uint64_t>(d.n_slices + 1) * d.n_chunks;
   }
   hipStream_t s = ctx->stream;
-  DLSM_CHECK(ctx->jobs.ensure(n_jobs));
-  DLSM_CHECK(ctx->starts.ensure(2 * n_jobs));
-  DLSM_CHECK(ctx->state.ensure(n_jobs));
-  DLSM_TRY(hipMemcpyAsync(ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs,
-                          hipMemcpyHostToDevice, s));
-  DLSM_TRY(hipMemcpyAsync(ctx->starts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs,
-                          hipMemcpyHostToDevice, s));
-  DLSM_TRY(hipMemsetAsync(ctx->state.p, 0, sizeof(JobState) * n_jobs, s));
+  const bool same = ctx->last_jobs.size() == hj.size() && ctx->last_starts == starts &&
+                    memcmp(ctx->last_jobs.data(), hj.data(), sizeof(FullJobDev) * n_jobs) == 0 &&
+                    ctx->jobs.cap >= static_cast<size_t>(n_jobs);
+  if (!same) {
+    DLSM_CHECK(ctx->jobs.ensure(n_jobs));
+    DLSM_CHECK(ctx->starts.ensure(2 * n_jobs));
+    DLSM_TRY(hipMemcpyAsync(ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs,
+                            hipMemcpyHostToDevice, s));
+    DLSM_TRY(hipMemcpyAsync(ctx->starts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs,
+                            hipMemcpyHostToDevice, s));
+    ctx->last_jobs = hj;
+    ctx->last_starts = starts;
+  }
+  DLSM_CHECK(ctx->dchunk.ensure(chunk));
+  DLSM_CHECK(ctx->jobL.ensure(n_jobs));
   const uint32_t* chunk0s = ctx->starts.p;
   const uint32_t* slice0s = ctx->starts.p + n_jobs;
   if (sliced_ok) {
     DLSM_CHECK(ctx->entries.ensure(entry));
     DLSM_CHECK(ctx->tab.ensure(tabw));
-    DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p,
+    DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p,
                                    ctx->entries.p, ctx->tab.p, lgR, mode, s));
-    DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, slice, ctx->state.p, ctx->entries.p,
+    DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, slice, ctx->dchunk.p, ctx->entries.p,
                                 ctx->tab.p, lgR, s));
   } else {
-    DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, mode, s));
-    DLSM_TRY(launch_full_zero(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, s));
-    DLSM_TRY(launch_full_scatter(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->state.p, mode, s));
+    DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, s));
+    DLSM_TRY(launch_full_zero(ctx->jobs.p, n_jobs, ctx->dchunk.p, ctx->jobL.p, s));
+    DLSM_TRY(launch_full_scatter(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->jobL.p, mode, s));
   }
   return DLSM_OK;
 }
@@ -607,14 +621,14 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   DLSM_CHECK(ctx->pos.ensure(n));
   DLSM_CHECK(ctx->smask.ensure(n));
   DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(S + 1) * nC));
-  // Enough (slice, part) workgroups to fill 256 CUs several times over, and no
-  // part smaller than one chunk group.
-  int parts = static_cast<int>(std::max<uint32_t>(1, 2048u / S));
-  parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 64)));
+  // (slice, part) workgroups: about one resident wave of workgroups (2 x 64 KiB
+  // slices per CU x 256 CUs), each part at least one 64-chunk group per wave.
+  int parts = static_cast<int>(std::max<uint32_t>(1, (512u + S / 2) / S));
+  parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 512)));
   const int lgR = 7;  // kProbeSliceLines
   DLSM_TRY(launch_probe_partition(kd, fs->L, fs->magic, lgR, S, ctx->entries.p, ctx->pos.p,
                                   ctx->tab.p, mode, s));
-  DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, n, ctx->entries.p,
+  DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ctx->entries.p,
                                ctx->tab.p, ctx->smask.p, parts, s));
   DLSM_TRY(launch_probe_unpermute(n, ctx->pos.p, ctx->smask.p, mask_dev, s));
   return DLSM_OK;

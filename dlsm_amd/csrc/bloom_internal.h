@@ -9,8 +9,9 @@
 
 namespace dlsm {
 
-// Key-load modes: K20 = fixed 20-byte keys at a 4-byte-aligned base (the
-// BASELINE shape), GENERIC = any fixed length / alignment or offsets.
+// Key-load modes: K20 = fixed 20-byte keys at a 16-byte-aligned base (the
+// BASELINE shape; staged through LDS with 16-byte loads), GENERIC = any fixed
+// length / alignment or offsets (per-thread aligned-dword loads).
 enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1 };
 
 struct KeyDesc {
@@ -33,13 +34,6 @@ struct FullJobDev {
   uint32_t slice0, n_slices;
   uint32_t L_spec, magic_spec;  // speculative line count (no duplicates) + fastmod magic
   int32_t k, bpk;
-};
-
-// Per-job device state written by the partition/count kernels.
-struct JobState {
-  unsigned long long distinct;  // consecutive-distinct hash count (AddKey dedup)
-  int32_t status;
-  uint32_t pad;
 };
 
 // A parsed full filter resident on the device (FullFilterBlockReader state).
@@ -66,21 +60,21 @@ constexpr int kProbeChunk = 8192;   // keys per partition chunk (probe)
 constexpr int kProbeSliceLines = 128;  // 128 lines x 512 B stacked = 64 KiB LDS
 
 // ---- launchers (bloom_kernels.hip) -----------------------------------------
-// All return hipError_t of the launch.
+// All return the hipError_t of the launch.  `dchunk` holds one
+// consecutive-distinct hash count per build chunk (written by the count /
+// partition kernels, summed per job by their consumers, so no per-call memset).
 hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                             uint32_t total_chunks, JobState* st, int mode, hipStream_t s);
-hipError_t launch_full_finalize(const FullJobDev* jobs, int n_jobs, JobState* st, hipStream_t s);
-hipError_t launch_full_zero(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                            uint32_t total_chunks, JobState* st, hipStream_t s);
+                             uint32_t total_chunks, uint32_t* dchunk, int mode, hipStream_t s);
+hipError_t launch_full_zero(const FullJobDev* jobs, int n_jobs, const uint32_t* dchunk,
+                            uint32_t* jobL, hipStream_t s);
 hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                               uint32_t total_chunks, JobState* st, int mode, hipStream_t s);
-
+                               uint32_t total_chunks, const uint32_t* jobL, int mode, hipStream_t s);
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                                 uint32_t total_chunks, JobState* st, uint32_t* entries,
+                                 uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
                                  uint32_t* tab, int lgR, int mode, hipStream_t s);
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
-                              uint32_t total_slices, JobState* st, const uint32_t* entries,
-                              const uint32_t* tab, int lgR, hipStream_t s);
+                              uint32_t total_slices, const uint32_t* dchunk,
+                              const uint32_t* entries, const uint32_t* tab, int lgR, hipStream_t s);
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
                                int mode, hipStream_t s);
@@ -90,7 +84,7 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                   uint32_t* tab, int mode, hipStream_t s);
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
-                               int lgR, uint32_t n_slices, uint32_t n_chunks, uint64_t n_keys,
+                               int lgR, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint32_t* tab, uint8_t* smask,
                                int parts, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,

@@ -107,9 +107,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// In-place exclusive scan of a[0, n) (n <= 4*kBlock) held in LDS.  Callers
-// synchronise before (a written by other threads); returns the total and ends
-// with a barrier.
+// In-place exclusive scan of a[0, n) (n <= 4*NT) held in LDS by an NT-thread
+// block.  Callers synchronise before (a written by other threads); returns the
+// total and ends with a barrier.
+template <int NT>
 __device__ uint32_t block_excl_scan_lds(uint32_t* a, int n, uint32_t* wsum) {
   const int t = threadIdx.x;
   uint32_t v[4];
@@ -126,7 +127,7 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, int n, uint32_t* wsum) {
   __syncthreads();
   uint32_t base = 0, total = 0;
 #pragma unroll
-  for (int ww = 0; ww < kBlock / 64; ww++) {
+  for (int ww = 0; ww < NT / 64; ww++) {
     const uint32_t x = wsum[ww];
     if (ww < w) base += x;
     total += x;
@@ -142,17 +143,6 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, int n, uint32_t* wsum) {
   return total;
 }
 
-__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* wsum) {
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = v;
-  __syncthreads();
-  uint32_t t = 0;
-#pragma unroll
-  for (int w = 0; w < kBlock / 64; w++) t += wsum[w];
-  __syncthreads();
-  return t;
-}
-
 // Largest j with starts[j] <= b (starts non-decreasing, starts[0] == 0).
 template <typename T>
 __device__ __forceinline__ int find_job(const T* starts, int n_jobs, T b) {
@@ -160,17 +150,6 @@ __device__ __forceinline__ int find_job(const T* starts, int n_jobs, T b) {
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (starts[mid] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// Largest c in [0, n) with pre[c] <= e (pre[0] == 0 <= e).
-__device__ __forceinline__ int seg_search(const uint32_t* pre, int n, uint32_t e) {
-  int lo = 0, hi = n - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (pre[mid] <= e) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -198,144 +177,290 @@ __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
 }
 
 // ---------------------------------------------------------------------------
-// Full filter build: hash + consecutive-dedup count (+ slice partition)
-// One workgroup per chunk of kBuildChunk keys of one job.
+// Chunk hashing.  Key i of a chunk (i = r*NT + t) is hashed by thread t into
+// h[r].  K20: the chunk's bytes are staged through LDS in tiles of
+// TILE = 4*NT keys with 16-byte, fully coalesced global loads (double-buffered
+// in registers), then each thread reads its key's five dwords from LDS (stride
+// 5 dwords: conflict-free).  GENERIC: each thread hashes its keys directly.
 // ---------------------------------------------------------------------------
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int NT>
+struct K20Tile {
+  static constexpr int kKeys = 4 * NT;               // keys per tile
+  static constexpr int kVec = kKeys * 20 / 16;       // uint4 per tile
+  static constexpr int kPer = kVec / NT;             // uint4 per thread (5)
+};
+
+template <int NT>
+__device__ __forceinline__ void k20_tile_fetch(const uint8_t* base, uint32_t nbytes, int q,
+                                               uint4 (&r)[K20Tile<NT>::kPer]) {
+  const uint4* b4 = reinterpret_cast<const uint4*>(base) + q * K20Tile<NT>::kVec;
+  const uint32_t tile_off = q * K20Tile<NT>::kVec * 16u;
+#pragma unroll
+  for (int v = 0; v < K20Tile<NT>::kPer; v++) {
+    const uint32_t u = v * NT + threadIdx.x;
+    const uint32_t off = tile_off + u * 16u;
+    if (off + 16u <= nbytes) {
+      const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b4 + u));
+      r[v] = make_uint4(x.x, x.y, x.z, x.w);
+    } else {
+      // tail: dword-granular (nbytes is a multiple of 4), never past the keys
+      const uint32_t* d = reinterpret_cast<const uint32_t*>(base + off);
+      r[v].x = off + 4u <= nbytes ? d[0] : 0u;
+      r[v].y = off + 8u <= nbytes ? d[1] : 0u;
+      r[v].z = off + 12u <= nbytes ? d[2] : 0u;
+      r[v].w = 0u;
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void k20_tile_store(uint4* lds, const uint4 (&r)[K20Tile<NT>::kPer]) {
+#pragma unroll
+  for (int v = 0; v < K20Tile<NT>::kPer; v++) lds[v * NT + threadIdx.x] = r[v];
+}
+
+__device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
+  uint32_t h = hash_init(20, kBloomSeed);
+  h = hash_word(h, w[0]);
+  h = hash_word(h, w[1]);
+  h = hash_word(h, w[2]);
+  h = hash_word(h, w[3]);
+  h = hash_word(h, w[4]);
+  return h;
+}
+
+// Hash keys [first, first+nk) of kd into h[PER] (key r*NT+t -> thread t, h[r]).
+// `tile` is LDS scratch of K20Tile<NT>::kVec uint4 (K20 only).
+template <int MODE, int NT, int PER>
+__device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, uint32_t nk,
+                                           uint4* tile, uint32_t (&h)[PER]) {
+  const int t = threadIdx.x;
+  if constexpr (MODE == KM_K20) {
+    constexpr int KPT = 4;
+    constexpr int NTILES = PER / KPT;
+    const uint8_t* base = kd.bytes + first * 20u;
+    const uint32_t nbytes = nk * 20u;
+    uint4 pre[K20Tile<NT>::kPer];
+    k20_tile_fetch<NT>(base, nbytes, 0, pre);
+#pragma unroll
+    for (int q = 0; q < NTILES; q++) {
+      k20_tile_store<NT>(tile, pre);
+      __syncthreads();
+      if (q + 1 < NTILES && (q + 1) * K20Tile<NT>::kKeys < static_cast<int>(nk))
+        k20_tile_fetch<NT>(base, nbytes, q + 1, pre);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
+#pragma unroll
+      for (int j = 0; j < KPT; j++) {
+        const int r = q * KPT + j;
+        h[r] = hash_k20_lds(w + 5 * (j * NT + t));
+      }
+      __syncthreads();
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + t;
+      h[r] = i < nk ? key_hash<KM_GENERIC>(kd, first + i) : 0u;
+    }
+  }
+}
+
+// Consecutive-distinct count of a chunk (AddKey, full_filter_block.cc:45-48):
+// key i counts unless its hash equals key i-1's.  `prev0` is the hash of the
+// key before the chunk, or ~h(key 0) for a job's first chunk (key 0 counts).
+template <int NT, int PER>
+__device__ __forceinline__ uint32_t chunk_distinct(const uint32_t (&h)[PER], uint32_t nk,
+                                                   uint32_t prev0, uint32_t* lastw,
+                                                   uint32_t* wsum) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  constexpr int NW = NT / 64;
+  if (lane == 63) {
+#pragma unroll
+    for (int r = 0; r < PER; r++) lastw[r * NW + w] = h[r];
+  }
+  __syncthreads();
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    uint32_t p = __shfl_up(h[r], 1, 64);
+    if (lane == 0) p = w > 0 ? lastw[r * NW + w - 1] : (r > 0 ? lastw[(r - 1) * NW + NW - 1] : prev0);
+    const uint32_t i = r * NT + t;
+    if (i < nk && h[r] != p) cnt++;
+  }
+  cnt = wave_sum(cnt);
+  if (lane == 0) wsum[w] = cnt;
+  __syncthreads();
+  uint32_t tot = 0;
+#pragma unroll
+  for (int q = 0; q < NW; q++) tot += wsum[q];
+  return tot;
+}
+
+// Largest lane l whose exclusive prefix excl[l] <= e (excl non-decreasing
+// across the wave).  Every lane must be active.
+__device__ __forceinline__ int wave_seg_find(uint32_t excl, uint32_t e) {
+  int lo = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    const uint32_t v = __shfl(excl, lo + step, 64);
+    if (v <= e) lo += step;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------------------
+// Full filter build, pass 1: hash + consecutive-dedup count (+ slice
+// partition).  One 512-thread workgroup per chunk of kBuildChunk keys of one
+// job.
+// ---------------------------------------------------------------------------
+constexpr int kPartBlock = 512;
+
 template <int MODE, bool PART>
-__global__ __launch_bounds__(kBlock) void full_partition_kernel(
+__global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
-    JobState* __restrict__ st, uint32_t* __restrict__ entries, uint32_t* __restrict__ tab,
+    uint32_t* __restrict__ dchunk, uint32_t* __restrict__ entries, uint32_t* __restrict__ tab,
     int lgR) {
   constexpr int C = kBuildChunk;
-  constexpr int PER = C / kBlock;
-  __shared__ uint32_t hs[C + 1];
+  constexpr int PER = C / kPartBlock;
+  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock>::kVec : 1];
   __shared__ uint32_t hist[kMaxSlices + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
+  __shared__ uint32_t wsum[kPartBlock / 64];
   __shared__ int sj;
   const int tid = threadIdx.x;
   if (tid == 0) sj = find_job(chunk0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
   __syncthreads();
-  const int j = sj;
-  const FullJobDev J = jobs[j];
+  const FullJobDev J = jobs[sj];
   const uint32_t c = blockIdx.x - J.chunk0;
   const uint64_t first = static_cast<uint64_t>(c) * C;
   const uint64_t left = J.keys.n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
 
   uint32_t h[PER];
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
-    h[r] = 0;
-    if (i < nk) {
-      h[r] = key_hash<MODE>(J.keys, first + i);
-      hs[i + 1] = h[r];
-    }
-  }
-  if (tid == 0) hs[0] = first > 0 ? key_hash<MODE>(J.keys, first - 1) : ~h[0];
-  __syncthreads();
-  // AddKey (full_filter_block.cc:45-48): a hash counts unless it equals the
-  // immediately preceding one; the job's key 0 always counts (hs[0] = ~h).
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
-    if (i < nk) cnt += (hs[i + 1] != hs[i]) ? 1u : 0u;
-  }
-  cnt = block_sum(cnt, wsum);
-  if (tid == 0) atomicAdd(&st[j].distinct, static_cast<unsigned long long>(cnt));
+  hash_chunk<MODE, kPartBlock, PER>(J.keys, first, nk, tile, h);
+  uint32_t prev0 = ~h[0];
+  if (first > 0) prev0 = key_hash<MODE == KM_K20 ? KM_K20 : KM_GENERIC>(J.keys, first - 1);
+  const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, __shfl(prev0, 0, 64), lastw, wsum);
+  if (tid == 0) dchunk[blockIdx.x] = cnt;
   if constexpr (!PART) return;
 
   const uint32_t S = J.n_slices;
-  for (uint32_t b = tid; b <= S; b += kBlock) hist[b] = 0;
+  for (uint32_t b = tid; b <= S; b += kPartBlock) hist[b] = 0;
   __syncthreads();
   uint32_t code[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
+    const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
       const uint32_t s = fastmod(h[r], J.L_spec, J.magic_spec) >> lgR;
-      const uint32_t rank = atomicAdd(&hist[s], 1u);
-      code[r] = (rank << 9) | s;
+      code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
     }
   }
   __syncthreads();
-  block_excl_scan_lds(hist, static_cast<int>(S + 1), wsum);
-  for (uint32_t b = tid; b <= S; b += kBlock)
+  block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
+  for (uint32_t b = tid; b <= S; b += kPartBlock)
     tab[J.tab0 + static_cast<uint64_t>(b) * J.n_chunks + c] = hist[b];
   uint32_t* ent = entries + J.entry0 + first;
 #pragma unroll
   for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
+    const uint32_t i = r * kPartBlock + tid;
     if (i < nk) ent[hist[code[r] & 511u] + (code[r] >> 9)] = h[r];
   }
 }
 
+// Sum of a job's per-chunk distinct counts (every thread gets the total).
+template <int NT>
+__device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint32_t* dchunk,
+                                                 uint32_t* wsum64) {
+  uint32_t lo = 0;
+  for (uint32_t c = threadIdx.x; c < J.n_chunks; c += NT) lo += dchunk[J.chunk0 + c];
+  // chunk counts are <= 4096, so a 32-bit partial per thread cannot overflow
+  // for < 2^20 chunks per thread; sum in 64 bits across threads
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t ws = wave_sum(lo);
+  if (lane == 0) wsum64[w] = ws;
+  __syncthreads();
+  uint64_t tot = 0;
+#pragma unroll
+  for (int q = 0; q < NT / 64; q++) tot += wsum64[q];
+  __syncthreads();
+  return tot;
+}
+
 // ---------------------------------------------------------------------------
-// Full filter build, sliced: one workgroup per (job, slice of 2^LGR lines).
+// Full filter build, pass 2 (sliced): one 512-thread workgroup per (job, slice
+// of 2^LGR lines).  The slice lives in LDS; each wave walks the slice's
+// segments of 64 chunks at a time (wave prefix scan + ds_bpermute search, 4
+// entries in flight per lane), ORs bits with ds_or, and the slice streams out
+// with 16-byte stores.
 // ---------------------------------------------------------------------------
+constexpr int kSliceBlock = 512;
+
 template <int LGR>
-__global__ __launch_bounds__(kBlock) void full_slice_kernel(
+__global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ slice0s, int n_jobs,
-    JobState* __restrict__ st, const uint32_t* __restrict__ entries,
+    const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ tab) {
   constexpr uint32_t R = 1u << LGR;
+  constexpr int U = 4;
+  constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
-  __shared__ uint32_t g_off[kBlock];
-  __shared__ uint32_t g_pre[kBlock + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t wsum[NW];
   __shared__ int sj;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) sj = find_job(slice0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
+  for (uint32_t w = tid; w < R * 16; w += kSliceBlock) sl[w] = 0;
   __syncthreads();
-  const int j = sj;
-  const FullJobDev J = jobs[j];
+  const FullJobDev J = jobs[sj];
   const uint32_t s = blockIdx.x - J.slice0;
+  const uint64_t distinct = job_distinct<kSliceBlock>(J, dchunk, wsum);
   uint32_t total_bits;
-  const uint32_t L = full_num_lines(st[j].distinct, J.bpk, &total_bits);
+  const uint32_t L = full_num_lines(distinct, J.bpk, &total_bits);
   const uint64_t len = static_cast<uint64_t>(total_bits / 8u) + 5u;
   if (len > J.out_cap) {
-    if (s == 0 && tid == 0) {
-      *J.out_len = 0;
-      st[j].status = -2;
-    }
+    if (s == 0 && tid == 0) *J.out_len = 0;
     return;
   }
   const uint32_t lo_line = s << LGR;
-  for (uint32_t w = tid; w < R * 16; w += kBlock) sl[w] = 0;
-  __syncthreads();
   if (L != 0 && lo_line < L) {
     const uint32_t magic = fastmod_magic(L);
     if (L == J.L_spec) {
       const uint32_t nC = J.n_chunks;
       const uint32_t* row0 = tab + J.tab0 + static_cast<uint64_t>(s) * nC;
       const uint32_t* row1 = row0 + nC;
-      for (uint32_t g0 = 0; g0 < nC; g0 += kBlock) {
-        const uint32_t gc = min(static_cast<uint32_t>(kBlock), nC - g0);
-        if (tid < gc) {
-          const uint32_t o0 = row0[g0 + tid];
-          g_off[tid] = o0;
-          g_pre[tid] = row1[g0 + tid] - o0;
-        } else {
-          g_pre[tid] = 0;
+      const uint32_t* ent = entries + J.entry0;
+      for (uint32_t g = wv * 64u; g < nC; g += NW * 64u) {
+        const uint32_t c = g + lane;
+        const uint32_t o0 = c < nC ? row0[c] : 0u;
+        const uint32_t cnt = c < nC ? row1[c] - o0 : 0u;
+        const uint32_t incl = wave_incl_scan(cnt);
+        const uint32_t excl = incl - cnt;
+        const uint32_t T = __shfl(incl, 63, 64);
+        for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
+          uint32_t hv[U];
+          bool ok[U];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const uint32_t e = e0 + u * 64u + lane;
+            ok[u] = e < T;
+            const uint32_t ec = ok[u] ? e : T - 1u;
+            const int li = wave_seg_find(excl, ec);
+            const uint64_t idx = static_cast<uint64_t>(g + li) * kBuildChunk +
+                                 __shfl(o0, li, 64) + (ec - __shfl(excl, li, 64));
+            hv[u] = ok[u] ? ent[idx] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], J.k);
         }
-        __syncthreads();
-        const uint32_t T = block_excl_scan_lds(g_pre, kBlock, wsum);
-        const uint32_t* ent = entries + J.entry0 + static_cast<uint64_t>(g0) * kBuildChunk;
-        for (uint32_t e = tid; e < T; e += kBlock) {
-          const int cc = seg_search(g_pre, static_cast<int>(gc), e);
-          const uint32_t hv =
-              ent[static_cast<uint64_t>(cc) * kBuildChunk + g_off[cc] + (e - g_pre[cc])];
-          const uint32_t li = fastmod(hv, L, magic) - lo_line;
-          lds_add_hash(sl + li * 16u, hv, J.k);
-        }
-        __syncthreads();
       }
     } else {
       // Duplicates lowered the line count below the speculative one: the
       // partition used the wrong modulus, so scan every hash of the job.
       const uint32_t* ent = entries + J.entry0;
-      for (uint64_t e = tid; e < J.keys.n; e += kBlock) {
+      for (uint64_t e = tid; e < J.keys.n; e += kSliceBlock) {
         const uint32_t hv = ent[e];
         const uint32_t line = fastmod(hv, L, magic);
         if ((line >> LGR) == s) lds_add_hash(sl + (line - lo_line) * 16u, hv, J.k);
@@ -345,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void full_slice_kernel(
     const uint32_t nl = min(R, L - lo_line);
     uint4* dst = reinterpret_cast<uint4*>(J.out + static_cast<uint64_t>(lo_line) * 64u);
     const uint4* src = reinterpret_cast<const uint4*>(sl);
-    for (uint32_t w = tid; w < nl * 4u; w += kBlock) dst[w] = src[w];
+    for (uint32_t w = tid; w < nl * 4u; w += kSliceBlock) dst[w] = src[w];
   }
   if (s == 0 && tid == 0) {
     write_trailer(J.out, L, J.k);
@@ -354,44 +479,48 @@ __global__ __launch_bounds__(kBlock) void full_slice_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Full filter build, direct path: zero + trailer, then global-atomic scatter.
+// Full filter build, direct path: count -> zero + trailer -> global-atomic
+// scatter.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void full_zero_kernel(const FullJobDev* __restrict__ jobs,
-                                                           JobState* __restrict__ st) {
+                                                           const uint32_t* __restrict__ dchunk,
+                                                           uint32_t* __restrict__ jobL) {
+  __shared__ uint32_t wsum[kBlock / 64];
   const FullJobDev J = jobs[blockIdx.y];
+  const uint64_t distinct = job_distinct<kBlock>(J, dchunk, wsum);
   uint32_t total_bits;
-  const uint32_t L = full_num_lines(st[blockIdx.y].distinct, J.bpk, &total_bits);
+  const uint32_t L = full_num_lines(distinct, J.bpk, &total_bits);
   const uint64_t len = static_cast<uint64_t>(total_bits / 8u) + 5u;
   if (len > J.out_cap) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       *J.out_len = 0;
-      st[blockIdx.y].status = -2;
+      jobL[blockIdx.y] = 0xffffffffu;
     }
     return;
   }
-  uint32_t* o = reinterpret_cast<uint32_t*>(J.out);
-  const uint64_t words = static_cast<uint64_t>(L) * 16u;
-  for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; w < words;
+  uint4* o = reinterpret_cast<uint4*>(J.out);
+  const uint64_t vecs = static_cast<uint64_t>(L) * 4u;
+  for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; w < vecs;
        w += static_cast<uint64_t>(gridDim.x) * kBlock)
-    o[w] = 0;
+    o[w] = make_uint4(0, 0, 0, 0);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     write_trailer(J.out, L, J.k);
     *J.out_len = len;
+    jobL[blockIdx.y] = L;
   }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void full_scatter_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
-    const JobState* __restrict__ st) {
+    const uint32_t* __restrict__ jobL) {
   __shared__ int sj;
   if (threadIdx.x == 0) sj = find_job(chunk0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
   __syncthreads();
   const int j = sj;
-  if (st[j].status != 0) return;
+  const uint32_t L = jobL[j];
+  if (L == 0 || L == 0xffffffffu) return;
   const FullJobDev J = jobs[j];
-  const uint32_t L = full_num_lines(st[j].distinct, J.bpk, nullptr);
-  if (L == 0) return;
   const uint32_t magic = fastmod_magic(L);
   const uint64_t first = static_cast<uint64_t>(blockIdx.x - J.chunk0) * kBuildChunk;
   const uint64_t end = min(J.keys.n, first + kBuildChunk);
@@ -442,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void probe_direct_kernel(const FilterDev* _
   const int mb = (F + 7) >> 3;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; i < kd.n;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    const uint32_t h = key_hash<MODE>(kd, i);
+    const uint32_t h = key_hash<MODE == KM_K20 ? KM_K20 : KM_GENERIC>(kd, i);
     for (int g = 0; g < mb; g++) {
       uint32_t m = 0;
       const int fe = min(F, 8 * g + 8);
@@ -468,38 +597,40 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
   }
 }
 
+// Pass 1: hash each lookup once and bucket it by slice inside its chunk.
+// entries[chunk region] = hashes grouped by slice; pos[i] = where key i went.
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void probe_partition_kernel(
+__global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint32_t* __restrict__ tab) {
   constexpr int C = kProbeChunk;
-  constexpr int PER = C / kBlock;
+  constexpr int PER = C / kPartBlock;
+  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock>::kVec : 1];
   __shared__ uint32_t hist[kMaxSlices + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t wsum[kPartBlock / 64];
   const int tid = threadIdx.x;
   const uint32_t c = blockIdx.x;
   const uint64_t first = static_cast<uint64_t>(c) * C;
   const uint64_t left = kd.n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
-  for (uint32_t b = tid; b <= S; b += kBlock) hist[b] = 0;
-  __syncthreads();
-  uint32_t h[PER], code[PER];
+  for (uint32_t b = tid; b <= S; b += kPartBlock) hist[b] = 0;
+  uint32_t h[PER];
+  hash_chunk<MODE, kPartBlock, PER>(kd, first, nk, tile, h);  // ends with a barrier
+  uint32_t code[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
+    const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
-      h[r] = key_hash<MODE>(kd, first + i);
       const uint32_t s = fastmod(h[r], L, magic) >> lgR;
-      const uint32_t rank = atomicAdd(&hist[s], 1u);
-      code[r] = (rank << 9) | s;
+      code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
     }
   }
   __syncthreads();
-  block_excl_scan_lds(hist, static_cast<int>(S + 1), wsum);
-  for (uint32_t b = tid; b <= S; b += kBlock) tab[static_cast<uint64_t>(b) * nC + c] = hist[b];
+  block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
+  for (uint32_t b = tid; b <= S; b += kPartBlock) tab[static_cast<uint64_t>(b) * nC + c] = hist[b];
 #pragma unroll
   for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kBlock + tid;
+    const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
       const uint32_t p = hist[code[r] & 511u] + (code[r] >> 9);
       entries[first + p] = h[r];
@@ -508,68 +639,108 @@ __global__ __launch_bounds__(kBlock) void probe_partition_kernel(
   }
 }
 
+// Pass 2: one 512-thread workgroup per (slice of 2^LGR stacked lines, part of
+// the chunks); the slice sits in LDS, waves walk the slice's segments of 64
+// chunks at a time with 4 hashes in flight per lane.  smask gets each key's
+// F-bit answer at the key's bucketed position.
 template <int LGR>
-__global__ __launch_bounds__(kBlock) void probe_slice_kernel(
+__global__ __launch_bounds__(kSliceBlock) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint32_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
-  __shared__ uint64_t sl[R * 64];
-  __shared__ uint32_t g_off[kBlock];
-  __shared__ uint32_t g_pre[kBlock + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
-  const int tid = threadIdx.x;
+  constexpr int U = 4;
+  constexpr int NW = kSliceBlock / 64;
+  __shared__ __attribute__((aligned(16))) uint64_t sl[R * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t s = blockIdx.x % S;
   const uint32_t p = blockIdx.x / S;
   const uint32_t lo_line = s << LGR;
   const uint32_t nl = min(R, L - lo_line);
-  const uint64_t* src = stacked + static_cast<uint64_t>(lo_line) * 64u;
-  for (uint32_t w = tid; w < nl * 64u; w += kBlock) sl[w] = src[w];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 64u);
+    uint4* dst = reinterpret_cast<uint4*>(sl);
+    for (uint32_t w = tid; w < nl * 32u; w += kSliceBlock) dst[w] = src[w];
+  }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint32_t* row0 = tab + static_cast<uint64_t>(s) * nC;
   const uint32_t* row1 = row0 + nC;
   __syncthreads();
-  for (uint32_t g0 = c_lo; g0 < c_hi; g0 += kBlock) {
-    const uint32_t gc = min(static_cast<uint32_t>(kBlock), c_hi - g0);
-    if (tid < gc) {
-      const uint32_t o0 = row0[g0 + tid];
-      g_off[tid] = o0;
-      g_pre[tid] = row1[g0 + tid] - o0;
-    } else {
-      g_pre[tid] = 0;
-    }
-    __syncthreads();
-    const uint32_t T = block_excl_scan_lds(g_pre, kBlock, wsum);
-    const uint64_t base = static_cast<uint64_t>(g0) * kProbeChunk;
-    for (uint32_t e = tid; e < T; e += kBlock) {
-      const int cc = seg_search(g_pre, static_cast<int>(gc), e);
-      const uint64_t idx = base + static_cast<uint64_t>(cc) * kProbeChunk + g_off[cc] + (e - g_pre[cc]);
-      uint32_t hv = entries[idx];
-      const uint32_t li = fastmod(hv, L, magic) - lo_line;
-      const uint64_t* line = sl + li * 64u;
-      const uint32_t delta = bloom_delta(hv);
-      uint64_t acc = 0x0101010101010101ull;
-      for (int q = 0; q < k; q++) {
-        const uint32_t bp = hv & 511u;
-        acc &= line[bp >> 3] >> (bp & 7u);
-        hv += delta;
+  for (uint32_t g = c_lo + wv * 64u; g < c_hi; g += NW * 64u) {
+    const uint32_t c = g + lane;
+    const uint32_t o0 = c < c_hi ? row0[c] : 0u;
+    const uint32_t cnt = c < c_hi ? row1[c] - o0 : 0u;
+    const uint32_t incl = wave_incl_scan(cnt);
+    const uint32_t excl = incl - cnt;
+    const uint32_t T = __shfl(incl, 63, 64);
+    for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
+      uint32_t hv[U];
+      uint64_t idx[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t e = e0 + u * 64u + lane;
+        ok[u] = e < T;
+        const uint32_t ec = ok[u] ? e : T - 1u;
+        const int li = wave_seg_find(excl, ec);
+        idx[u] = static_cast<uint64_t>(g + li) * kProbeChunk + __shfl(o0, li, 64) +
+                 (ec - __shfl(excl, li, 64));
+        hv[u] = ok[u] ? entries[idx[u]] : 0u;
       }
-      acc &= 0x0101010101010101ull;
-      smask[idx] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (!ok[u]) continue;
+        uint32_t x = hv[u];
+        const uint64_t* ln = sl + (fastmod(x, L, magic) - lo_line) * 64u;
+        const uint32_t delta = bloom_delta(x);
+        uint64_t acc = 0x0101010101010101ull;
+        for (int q = 0; q < k; q++) {
+          const uint32_t bp = x & 511u;
+          acc &= ln[bp >> 3] >> (bp & 7u);
+          x += delta;
+        }
+        acc &= 0x0101010101010101ull;
+        smask[idx[u]] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
+      }
     }
-    __syncthreads();
   }
 }
 
+// Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
+// (16-byte loads), gather them back to key order through pos (16-byte loads
+// of 8 positions), store 8 answers per lane.
 __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
                                                                  const uint16_t* __restrict__ pos,
                                                                  const uint8_t* __restrict__ smask,
                                                                  uint8_t* __restrict__ mask) {
-  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    const uint64_t base = i & ~static_cast<uint64_t>(kProbeChunk - 1);
-    mask[i] = smask[base + pos[i]];
+  constexpr int C = kProbeChunk;
+  __shared__ __attribute__((aligned(16))) uint8_t sm[C];
+  const int tid = threadIdx.x;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * C;
+  const uint64_t left = n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+  const uint32_t nvec = nk / 16u;
+  const uint4* s4 = reinterpret_cast<const uint4*>(smask + first);
+  for (uint32_t v = tid; v < nvec; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
+  for (uint32_t b = nvec * 16u + tid; b < nk; b += kBlock) sm[b] = smask[first + b];
+  __syncthreads();
+  for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
+    if (i0 + 8u <= nk) {
+      const uint4 pv = *reinterpret_cast<const uint4*>(pos + first + i0);
+      const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        lo |= uint32_t(sm[pw[q] & 0xffffu]) << (16 * q);
+        lo |= uint32_t(sm[pw[q] >> 16]) << (16 * q + 8);
+        hi |= uint32_t(sm[pw[q + 2] & 0xffffu]) << (16 * q);
+        hi |= uint32_t(sm[pw[q + 2] >> 16]) << (16 * q + 8);
+      }
+      *reinterpret_cast<uint2*>(mask + first + i0) = make_uint2(lo, hi);
+    } else {
+      for (uint32_t i = i0; i < nk; i++) mask[first + i] = sm[pos[first + i]];
+    }
   }
 }
 
@@ -641,67 +812,60 @@ inline unsigned grid_for(uint64_t n, unsigned cap = 256u * 16u) {
 // Launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                             uint32_t total_chunks, JobState* st, int mode, hipStream_t s) {
+                             uint32_t total_chunks, uint32_t* dchunk, int mode, hipStream_t s) {
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
-    full_partition_kernel<KM_K20, false><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, st,
+    full_partition_kernel<KM_K20, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                           nullptr, nullptr, 0);
   else
-    full_partition_kernel<KM_GENERIC, false><<<total_chunks, kBlock, 0, s>>>(
-        jobs, chunk0s, n_jobs, st, nullptr, nullptr, 0);
+    full_partition_kernel<KM_GENERIC, false><<<total_chunks, kPartBlock, 0, s>>>(
+        jobs, chunk0s, n_jobs, dchunk, nullptr, nullptr, 0);
   return hipGetLastError();
 }
 
-hipError_t launch_full_zero(const FullJobDev* jobs, const uint32_t*, int n_jobs, uint32_t,
-                            JobState* st, hipStream_t s) {
+hipError_t launch_full_zero(const FullJobDev* jobs, int n_jobs, const uint32_t* dchunk,
+                            uint32_t* jobL, hipStream_t s) {
   if (n_jobs == 0) return hipSuccess;
-  full_zero_kernel<<<dim3(64, n_jobs), kBlock, 0, s>>>(jobs, st);
+  full_zero_kernel<<<dim3(64, n_jobs), kBlock, 0, s>>>(jobs, dchunk, jobL);
   return hipGetLastError();
 }
 
 hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                               uint32_t total_chunks, JobState* st, int mode, hipStream_t s) {
+                               uint32_t total_chunks, const uint32_t* jobL, int mode, hipStream_t s) {
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
-    full_scatter_kernel<KM_K20><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, st);
+    full_scatter_kernel<KM_K20><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
   else
-    full_scatter_kernel<KM_GENERIC><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, st);
+    full_scatter_kernel<KM_GENERIC><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
   return hipGetLastError();
 }
 
-hipError_t launch_full_finalize(const FullJobDev*, int, JobState*, hipStream_t) {
-  return hipSuccess;
-}
-
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                                 uint32_t total_chunks, JobState* st, uint32_t* entries,
+                                 uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
                                  uint32_t* tab, int lgR, int mode, hipStream_t s) {
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
-    full_partition_kernel<KM_K20, true><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, st,
+    full_partition_kernel<KM_K20, true><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                          entries, tab, lgR);
   else
-    full_partition_kernel<KM_GENERIC, true><<<total_chunks, kBlock, 0, s>>>(
-        jobs, chunk0s, n_jobs, st, entries, tab, lgR);
+    full_partition_kernel<KM_GENERIC, true><<<total_chunks, kPartBlock, 0, s>>>(
+        jobs, chunk0s, n_jobs, dchunk, entries, tab, lgR);
   return hipGetLastError();
 }
 
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
-                              uint32_t total_slices, JobState* st, const uint32_t* entries,
-                              const uint32_t* tab, int lgR, hipStream_t s) {
+                              uint32_t total_slices, const uint32_t* dchunk,
+                              const uint32_t* entries, const uint32_t* tab, int lgR, hipStream_t s) {
   if (total_slices == 0) return hipSuccess;
   switch (lgR) {
-    case 8:
-      full_slice_kernel<8><<<total_slices, kBlock, 0, s>>>(jobs, slice0s, n_jobs, st, entries, tab);
-      break;
     case 9:
-      full_slice_kernel<9><<<total_slices, kBlock, 0, s>>>(jobs, slice0s, n_jobs, st, entries, tab);
+      full_slice_kernel<9><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
       break;
     case 10:
-      full_slice_kernel<10><<<total_slices, kBlock, 0, s>>>(jobs, slice0s, n_jobs, st, entries, tab);
+      full_slice_kernel<10><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
       break;
     case 11:
-      full_slice_kernel<11><<<total_slices, kBlock, 0, s>>>(jobs, slice0s, n_jobs, st, entries, tab);
+      full_slice_kernel<11><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
       break;
     default:
       return hipErrorInvalidValue;
@@ -733,29 +897,29 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
   const uint32_t nC = static_cast<uint32_t>((keys.n + kProbeChunk - 1) / kProbeChunk);
   if (nC == 0) return hipSuccess;
   if (mode == KM_K20)
-    probe_partition_kernel<KM_K20><<<nC, kBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K20><<<nC, kPartBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                          entries, pos, tab);
   else
-    probe_partition_kernel<KM_GENERIC><<<nC, kBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_GENERIC><<<nC, kPartBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                              entries, pos, tab);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR,
-                               uint32_t n_slices, uint32_t n_chunks, uint64_t,
-                               const uint32_t* entries, const uint32_t* tab, uint8_t* smask,
-                               int parts, hipStream_t s) {
+                               uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
+                               const uint32_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (lgR != 7) return hipErrorInvalidValue;
-  probe_slice_kernel<7><<<n_slices * parts, kBlock, 0, s>>>(stacked, L, magic, k, n_slices,
-                                                            n_chunks, entries, tab, smask, parts);
+  probe_slice_kernel<7><<<n_slices * parts, kSliceBlock, 0, s>>>(stacked, L, magic, k, n_slices,
+                                                                 n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                   uint8_t* mask, hipStream_t s) {
   if (n_keys == 0) return hipSuccess;
-  probe_unpermute_kernel<<<grid_for(n_keys, 256u * 64u), kBlock, 0, s>>>(n_keys, pos, smask, mask);
+  const uint64_t nC = (n_keys + kProbeChunk - 1) / kProbeChunk;
+  probe_unpermute_kernel<<<static_cast<unsigned>(nC), kBlock, 0, s>>>(n_keys, pos, smask, mask);
   return hipGetLastError();
 }
 

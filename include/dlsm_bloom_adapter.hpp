@@ -1,0 +1,219 @@
+// dlsm_bloom_adapter.hpp -- header-only C++ mirror of dLSM's filter classes
+// over the C ABI (dlsm_bloom.h).  Same class and method names, argument
+// meaning and call order as the reference, so a TableBuilder / Table can swap
+// them in (INTEGRATION.md shows the reference-side edit):
+//
+//   FullFilterBlockBuilder  table/full_filter_block.h:33-70
+//       (RestartBlock AddKey*)* Finish; Reset; Move_buffer; public `result`
+//   FullFilterBlockReader   table/full_filter_block.h:71-94
+//       ctor parses metadata; KeyMayMatch; + KeysMayMatch (batch)
+//   BloomFilterPolicy       include/TimberSaw/filter_policy.h:31-55, util/bloom.cc
+//       Name / CreateFilter / KeyMayMatch
+//
+// No exceptions (the reference builds with -fno-exceptions): failures are
+// reported through status().  All compute runs on the GPU behind the ABI.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dlsm_bloom.h"
+
+namespace dlsm_adapter {
+
+// Byte view with the reference Slice's surface used on this path
+// (include/TimberSaw/slice.h:27-103): data/size/Reset/append.
+class Slice {
+ public:
+  Slice() : data_(""), size_(0) {}
+  Slice(const char* d, size_t n) : data_(d), size_(n) {}
+  Slice(const std::string& s) : data_(s.data()), size_(s.size()) {}  // NOLINT
+  const char* data() const { return data_; }
+  size_t size() const { return size_; }
+  bool empty() const { return size_ == 0; }
+  void Reset(const char* d, size_t n) {
+    data_ = d;
+    size_ = n;
+  }
+  // Unchecked, like the reference (slice.h:93-97).
+  void append(const char* p, size_t n) {
+    memcpy(const_cast<char*>(data_) + size_, p, n);
+    size_ += n;
+  }
+  std::string ToString() const { return std::string(data_, size_); }
+
+ private:
+  const char* data_;
+  size_t size_;
+};
+
+// Stand-in for the ibv_mr the reference builder borrows: the filter slot.
+struct FilterSlot {
+  void* addr;
+  size_t length;
+};
+
+class FullFilterBlockBuilder {
+ public:
+  FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx)
+      : local_mr_(mr), bits_per_key_(bits_per_key),
+        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx),
+        result(static_cast<char*>(mr->addr), 0) {
+    offsets_.push_back(0);
+  }
+  FullFilterBlockBuilder(const FullFilterBlockBuilder&) = delete;
+  FullFilterBlockBuilder& operator=(const FullFilterBlockBuilder&) = delete;
+
+  // full_filter_block.cc:30-33 -- drops the pending keys.
+  void RestartBlock(uint64_t /*block_offset*/) {
+    keys_.clear();
+    offsets_.assign(1, 0);
+  }
+  // full_filter_block.cc:39-49 -- the GPU applies the consecutive-hash dedup.
+  void AddKey(const Slice& key) {
+    keys_.append(key.data(), key.size());
+    offsets_.push_back(keys_.size());
+  }
+  // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
+  // buffer (the slot, or the buffer given to Move_buffer).
+  void Finish() {
+    dlsm_build_job job;
+    job.keys.bytes = reinterpret_cast<const uint8_t*>(keys_.data());
+    job.keys.offsets = offsets_.data();
+    job.keys.key_len = 0;
+    job.keys.reserved = 0;
+    job.keys.n = offsets_.size() - 1;
+    job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
+    job.out_cap = local_mr_->length - static_cast<size_t>(result.data() - static_cast<char*>(local_mr_->addr));
+    if (result.data() < static_cast<char*>(local_mr_->addr) ||
+        result.data() >= static_cast<char*>(local_mr_->addr) + local_mr_->length)
+      job.out_cap = moved_cap_;
+    uint64_t len = 0;
+    status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
+    keys_.clear();
+    offsets_.assign(1, 0);
+    result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
+  }
+  void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
+  // Output goes to p from now on (full_filter_block.cc:146-148); cap is the
+  // size of p's buffer (the reference does not check; we do).
+  void Move_buffer(const char* p, size_t cap = SIZE_MAX) {
+    result.Reset(p, 0);
+    moved_cap_ = cap;
+  }
+  int num_probes() const { return num_probes_; }
+  int status() const { return status_; }
+
+ private:
+  FilterSlot* local_mr_;
+  int bits_per_key_;
+  int num_probes_;
+  dlsm_ctx* ctx_;
+  std::string keys_;
+  std::vector<uint64_t> offsets_;
+  size_t moved_cap_ = SIZE_MAX;
+  int status_ = DLSM_OK;
+
+ public:
+  Slice result;  // Filter data computed so far
+};
+
+class FullFilterBlockReader {
+ public:
+  // full_filter_block.cc:186-252: corrupt metadata -> status() ==
+  // DLSM_E_CORRUPT (the reference exit(1)s).
+  FullFilterBlockReader(const Slice& contents, dlsm_ctx* ctx) : filter_content(contents), ctx_(ctx) {
+    status_ = dlsm_bloom_full_parse(reinterpret_cast<const uint8_t*>(contents.data()),
+                                    contents.size(), &num_probes_, &num_lines_, &log2_line_);
+    if (status_ != DLSM_OK) return;
+    const uint8_t* f = reinterpret_cast<const uint8_t*>(contents.data());
+    const uint64_t len = contents.size();
+    status_ = dlsm_filterset_create(ctx_, &f, &len, 1, 0, &fs_);
+  }
+  ~FullFilterBlockReader() {
+    if (fs_) dlsm_filterset_destroy(fs_);
+  }
+  FullFilterBlockReader(const FullFilterBlockReader&) = delete;
+  FullFilterBlockReader& operator=(const FullFilterBlockReader&) = delete;
+
+  bool KeyMayMatch(const Slice& key) {
+    uint8_t m = 0;
+    return KeysMayMatch(&key, 1, &m) == DLSM_OK && m != 0;
+  }
+  // Batch form (the GPU's shape): out[i] = 1 if keys[i] may match.
+  int KeysMayMatch(const Slice* keys, size_t n, uint8_t* out) {
+    if (status_ != DLSM_OK) return status_;
+    std::string bytes;
+    std::vector<uint64_t> offs(1, 0);
+    for (size_t i = 0; i < n; i++) {
+      bytes.append(keys[i].data(), keys[i].size());
+      offs.push_back(bytes.size());
+    }
+    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0, n};
+    return dlsm_bloom_full_probe(ctx_, fs_, &ks, out);
+  }
+  int status() const { return status_; }
+  int num_probes() const { return num_probes_; }
+  uint32_t num_lines() const { return num_lines_; }
+
+  Slice filter_content;
+
+ private:
+  dlsm_ctx* ctx_;
+  dlsm_filterset* fs_ = nullptr;
+  int num_probes_ = 0;
+  uint32_t num_lines_ = 0;
+  int log2_line_ = 0;
+  int status_ = DLSM_OK;
+};
+
+// The legacy-format policy (util/bloom.cc).  Name() keeps the reference's
+// format identity string.
+class BloomFilterPolicy {
+ public:
+  BloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx) : bits_per_key_(bits_per_key), ctx_(ctx) {}
+  const char* Name() const { return "TimberSaw.BuiltinBloomFilter2"; }
+
+  // Append a filter summarising keys[0, n) to *dst (util/bloom.cc:25-55).
+  void CreateFilter(const Slice* keys, int n, Slice* dst) const {
+    std::string bytes;
+    std::vector<uint64_t> offs(1, 0);
+    for (int i = 0; i < n; i++) {
+      bytes.append(keys[i].data(), keys[i].size());
+      offs.push_back(bytes.size());
+    }
+    uint64_t need = 0;
+    dlsm_bloom_legacy_size(static_cast<uint64_t>(n < 0 ? 0 : n), bits_per_key_, &need);
+    dlsm_build_job job;
+    job.keys = dlsm_keyset{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0,
+                           static_cast<uint64_t>(n < 0 ? 0 : n)};
+    job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(dst->data())) + dst->size();
+    job.out_cap = need;
+    uint64_t len = 0;
+    last_status_ = dlsm_bloom_legacy_build(ctx_, &job, 1, bits_per_key_, &len);
+    if (last_status_ == DLSM_OK) dst->Reset(dst->data(), dst->size() + len);
+  }
+  bool KeyMayMatch(const Slice& key, const Slice& filter) const {
+    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(key.data()), nullptr,
+                   static_cast<uint32_t>(key.size()), 0, 1};
+    uint8_t r = 0;
+    if (key.size() == 0) {
+      static const uint8_t z = 0;
+      ks.bytes = &z;
+    }
+    last_status_ = dlsm_bloom_legacy_probe(ctx_, reinterpret_cast<const uint8_t*>(filter.data()),
+                                           filter.size(), &ks, &r);
+    return last_status_ == DLSM_OK && r != 0;
+  }
+  int status() const { return last_status_; }
+
+ private:
+  int bits_per_key_;
+  dlsm_ctx* ctx_;
+  mutable int last_status_ = DLSM_OK;
+};
+
+}  // namespace dlsm_adapter

@@ -1,0 +1,119 @@
+// GPU test of the C++ adapter (include/dlsm_bloom_adapter.hpp) -- the classes a
+// reference TableBuilder / Table would call -- against the oracle (test
+// infrastructure).  Built and run by tests/test_gpu_adapter.py.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "dlsm_bloom_adapter.hpp"
+
+extern "C" {
+int64_t orc_full_build(const uint8_t*, const uint64_t*, uint32_t, uint64_t, int, uint8_t*, uint64_t);
+int orc_full_key_may_match(const uint8_t*, uint64_t, const uint8_t*, size_t);
+int64_t orc_legacy_build(const uint8_t*, const uint64_t*, uint32_t, uint64_t, int, uint8_t*, uint64_t);
+int orc_legacy_key_may_match(const uint8_t*, uint64_t, const uint8_t*, size_t);
+void orc_dbbench_key(uint64_t v, int key_size, uint8_t* out);
+}
+
+#define CHECK(c)                                                   \
+  do {                                                             \
+    if (!(c)) {                                                    \
+      std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);      \
+      return 1;                                                    \
+    }                                                              \
+  } while (0)
+
+using dlsm_adapter::Slice;
+
+int main() {
+  dlsm_ctx* ctx = nullptr;
+  CHECK(dlsm_ctx_create(0, &ctx) == DLSM_OK);
+  // ---- FullFilterBlockBuilder: the TableBuilder call shape ----
+  for (int n : {0, 1, 52, 5000, 153846}) {
+    std::vector<char> slot(256 * 1024, 0);  // FilterChunk slot (options.h:28), zeroed
+    dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx);
+    b.RestartBlock(0);
+    std::string flat;
+    std::vector<uint64_t> offs{0};
+    for (int i = 0; i < n; i++) {
+      uint8_t k[20];
+      orc_dbbench_key(static_cast<uint64_t>(i) * 3 + 1, 20, k);
+      b.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+      flat.append(reinterpret_cast<char*>(k), 20);
+      offs.push_back(flat.size());
+    }
+    b.Finish();
+    CHECK(b.status() == DLSM_OK);
+    std::vector<uint8_t> want(256 * 1024, 0);
+    int64_t wl = orc_full_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0, n, 10,
+                                want.data(), want.size());
+    CHECK(wl > 0 && static_cast<int64_t>(b.result.size()) == wl);
+    CHECK(std::memcmp(b.result.data(), want.data(), wl) == 0);
+    CHECK(b.result.data() == slot.data());
+    // ---- FullFilterBlockReader ----
+    if (n > 0) {
+      dlsm_adapter::FullFilterBlockReader r(b.result, ctx);
+      CHECK(r.status() == DLSM_OK && r.num_probes() == 6);
+      std::vector<Slice> q;
+      std::vector<std::string> qs;
+      for (int i = 0; i < 3000; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i), 20, k);
+        qs.emplace_back(reinterpret_cast<char*>(k), 20);
+      }
+      for (auto& s : qs) q.emplace_back(s);
+      std::vector<uint8_t> got(q.size());
+      CHECK(r.KeysMayMatch(q.data(), q.size(), got.data()) == DLSM_OK);
+      for (size_t i = 0; i < q.size(); i++)
+        CHECK(got[i] == orc_full_key_may_match(want.data(), wl,
+                                               reinterpret_cast<const uint8_t*>(q[i].data()), 20));
+      CHECK(r.KeyMayMatch(Slice(flat.data(), 20)));
+    }
+    b.Reset();
+    CHECK(b.result.size() == 0);
+  }
+  // corrupt filter -> status, not exit(1)
+  {
+    char bad[69] = {0};
+    bad[65] = 1;  // k byte 0
+    dlsm_adapter::FullFilterBlockReader r(Slice(bad, sizeof(bad)), ctx);
+    CHECK(r.status() == DLSM_E_CORRUPT);
+    CHECK(!r.KeyMayMatch(Slice("x", 1)));
+  }
+  // ---- BloomFilterPolicy (legacy format) ----
+  {
+    dlsm_adapter::BloomFilterPolicy pol(10, ctx);
+    CHECK(std::strcmp(pol.Name(), "TimberSaw.BuiltinBloomFilter2") == 0);
+    std::vector<char> buf(64 * 1024, 0);
+    Slice dst(buf.data(), 0);
+    const char* prefix = "hdr";
+    dst.append(prefix, 3);  // CreateFilter appends after existing content
+    std::vector<std::string> ks = {"hello", "world", "", "a", "0123456789abcdef0123"};
+    std::vector<Slice> keys(ks.begin(), ks.end());
+    pol.CreateFilter(keys.data(), static_cast<int>(keys.size()), &dst);
+    CHECK(pol.status() == DLSM_OK);
+    std::string flat;
+    std::vector<uint64_t> offs{0};
+    for (auto& s : ks) {
+      flat += s;
+      offs.push_back(flat.size());
+    }
+    std::vector<uint8_t> want(1024, 0);
+    int64_t wl = orc_legacy_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0,
+                                  ks.size(), 10, want.data(), want.size());
+    CHECK(static_cast<int64_t>(dst.size()) == 3 + wl);
+    CHECK(std::memcmp(dst.data(), "hdr", 3) == 0);
+    CHECK(std::memcmp(dst.data() + 3, want.data(), wl) == 0);
+    Slice filt(dst.data() + 3, wl);
+    for (auto& s : ks) CHECK(pol.KeyMayMatch(Slice(s), filt));
+    for (const char* q : {"x", "foo", "hello!", "zz"})
+      CHECK(pol.KeyMayMatch(Slice(q, std::strlen(q)), filt) ==
+            (orc_legacy_key_may_match(want.data(), wl, reinterpret_cast<const uint8_t*>(q),
+                                      std::strlen(q)) != 0));
+  }
+  dlsm_ctx_destroy(ctx);
+  std::printf("OK adapter\n");
+  return 0;
+}
