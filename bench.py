@@ -64,6 +64,7 @@ def main():
     import torch
 
     import dlsm_amd
+    from dlsm_amd import sharding as SH
     from dlsm_amd import workload as W
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -88,7 +89,8 @@ def main():
     with torch.cuda.stream(stream):
         tables, outs = [], []
         for s in range(T):
-            v = torch.arange(N, device=dev, dtype=torch.int64) * T + (s + rank * T * N)
+            first, step = SH.table_values(rank, s, T, N)
+            v = torch.arange(N, device=dev, dtype=torch.int64) * step + first
             tables.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), N, 20))
             outs.append(torch.zeros(dlsm_amd.full_size(N, bpk)[0], dtype=torch.uint8, device=dev))
         lens = torch.zeros(T, dtype=torch.uint64, device=dev)
@@ -104,7 +106,7 @@ def main():
     fl = flens.cpu().numpy()
     filters = [fouts[f][: int(fl[f])] for f in range(F)]
     fs = ctx.filterset(filters, on_device=True)
-    qv = W.mt19937_64(1000 + rank, Q) % np.uint64(2 * F * N)
+    qv = W.mt19937_64(SH.lookup_seed(rank), Q) % np.uint64(2 * F * N)
     qkeys = W.dbbench_keys_torch(torch.from_numpy(qv.astype(np.int64)).to(dev))
     qk = dlsm_amd.Keys(qkeys, Q, 20)
     mask = torch.empty(Q * fs.mask_bytes, dtype=torch.uint8, device=dev)
@@ -137,10 +139,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = SH.max_over_ranks(elapsed, dist, dev)
     build_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
     probe_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
 

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -73,6 +74,7 @@ struct dlsm_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   int path = 0;
+  uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint32_t> tab;
@@ -258,6 +260,8 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
     return from_hip(e);
   }
   ctx->stream = ctx->own;
+  ctx->probe_round = 16ull << 20;
+  if (const char* e = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(e, nullptr, 10);
   *out = ctx;
   return DLSM_OK;
 }
@@ -615,22 +619,36 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
     return DLSM_OK;
   }
+  // Rounds: the bucketed intermediates (4 B hash + 2 B position + 1 B answer
+  // per key) of one round stay resident in the 256 MiB Infinity Cache, and the
+  // next round overwrites the same lines, so they never stream to HBM.
   const uint64_t n = keys->n;
-  const uint32_t nC = ceil_div_u32(n, kProbeChunk);
-  DLSM_CHECK(ctx->entries.ensure(n));
-  DLSM_CHECK(ctx->pos.ensure(n));
-  DLSM_CHECK(ctx->smask.ensure(n));
-  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(S + 1) * nC));
-  // (slice, part) workgroups: about one resident wave of workgroups (2 x 64 KiB
-  // slices per CU x 256 CUs), each part at least one 64-chunk group per wave.
-  int parts = static_cast<int>(std::max<uint32_t>(1, (512u + S / 2) / S));
-  parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 512)));
+  uint64_t round = ctx->probe_round ? ctx->probe_round : n;
+  round = std::max<uint64_t>(kProbeChunk, (round / kProbeChunk) * kProbeChunk);
+  const uint64_t rk = std::min(round, n);
+  const uint32_t nCmax = ceil_div_u32(rk, kProbeChunk);
+  DLSM_CHECK(ctx->entries.ensure(rk));
+  DLSM_CHECK(ctx->pos.ensure(rk));
+  DLSM_CHECK(ctx->smask.ensure(rk));
+  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(S + 1) * nCmax));
   const int lgR = 7;  // kProbeSliceLines
-  DLSM_TRY(launch_probe_partition(kd, fs->L, fs->magic, lgR, S, ctx->entries.p, ctx->pos.p,
-                                  ctx->tab.p, mode, s));
-  DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ctx->entries.p,
-                               ctx->tab.p, ctx->smask.p, parts, s));
-  DLSM_TRY(launch_probe_unpermute(n, ctx->pos.p, ctx->smask.p, mask_dev, s));
+  for (uint64_t r0 = 0; r0 < n; r0 += round) {
+    const uint64_t nr = std::min(round, n - r0);
+    const uint32_t nC = ceil_div_u32(nr, kProbeChunk);
+    KeyDesc kr = kd;
+    kr.n = nr;
+    if (kd.offsets) kr.offsets = kd.offsets + r0;
+    else kr.bytes = kd.bytes + r0 * kd.key_len;
+    // (slice, part) workgroups: about one resident wave of workgroups (2 x 64
+    // KiB slices per CU x 256 CUs), each part at least one 64-chunk group per wave.
+    int parts = static_cast<int>(std::max<uint32_t>(1, (512u + S / 2) / S));
+    parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 1024)));
+    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ctx->entries.p, ctx->pos.p,
+                                    ctx->tab.p, mode, s));
+    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ctx->entries.p,
+                                 ctx->tab.p, ctx->smask.p, parts, s));
+    DLSM_TRY(launch_probe_unpermute(nr, ctx->pos.p, ctx->smask.p, mask_dev + r0, s));
+  }
   return DLSM_OK;
 }
 

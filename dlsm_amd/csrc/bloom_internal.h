@@ -56,7 +56,7 @@ struct LegacyJobDev {
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
 constexpr int kBuildChunk = 4096;   // keys per partition chunk (build)
-constexpr int kProbeChunk = 8192;   // keys per partition chunk (probe)
+constexpr int kProbeChunk = 4096;   // keys per partition chunk (probe)
 constexpr int kProbeSliceLines = 128;  // 128 lines x 512 B stacked = 64 KiB LDS
 
 // ---- launchers (bloom_kernels.hip) -----------------------------------------

@@ -185,21 +185,23 @@ __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int NT>
+template <int NT, int KPT>
 struct K20Tile {
-  static constexpr int kKeys = 4 * NT;               // keys per tile
-  static constexpr int kVec = kKeys * 20 / 16;       // uint4 per tile
-  static constexpr int kPer = kVec / NT;             // uint4 per thread (5)
+  static constexpr int kKeys = KPT * NT;                 // keys per tile
+  static constexpr int kVec = kKeys * 20 / 16;           // uint4 per tile
+  static constexpr int kPer = (kVec + NT - 1) / NT;      // uint4 per thread
 };
 
-template <int NT>
+template <int NT, int KPT>
 __device__ __forceinline__ void k20_tile_fetch(const uint8_t* base, uint32_t nbytes, int q,
-                                               uint4 (&r)[K20Tile<NT>::kPer]) {
-  const uint4* b4 = reinterpret_cast<const uint4*>(base) + q * K20Tile<NT>::kVec;
-  const uint32_t tile_off = q * K20Tile<NT>::kVec * 16u;
+                                               uint4 (&r)[K20Tile<NT, KPT>::kPer]) {
+  using TL = K20Tile<NT, KPT>;
+  const uint4* b4 = reinterpret_cast<const uint4*>(base) + q * TL::kVec;
+  const uint32_t tile_off = q * TL::kVec * 16u;
 #pragma unroll
-  for (int v = 0; v < K20Tile<NT>::kPer; v++) {
+  for (int v = 0; v < TL::kPer; v++) {
     const uint32_t u = v * NT + threadIdx.x;
+    if (TL::kVec % NT != 0 && u >= static_cast<uint32_t>(TL::kVec)) break;
     const uint32_t off = tile_off + u * 16u;
     if (off + 16u <= nbytes) {
       const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b4 + u));
@@ -215,10 +217,15 @@ __device__ __forceinline__ void k20_tile_fetch(const uint8_t* base, uint32_t nby
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void k20_tile_store(uint4* lds, const uint4 (&r)[K20Tile<NT>::kPer]) {
+template <int NT, int KPT>
+__device__ __forceinline__ void k20_tile_store(uint4* lds, const uint4 (&r)[K20Tile<NT, KPT>::kPer]) {
+  using TL = K20Tile<NT, KPT>;
 #pragma unroll
-  for (int v = 0; v < K20Tile<NT>::kPer; v++) lds[v * NT + threadIdx.x] = r[v];
+  for (int v = 0; v < TL::kPer; v++) {
+    const uint32_t u = v * NT + threadIdx.x;
+    if (TL::kVec % NT != 0 && u >= static_cast<uint32_t>(TL::kVec)) break;
+    lds[u] = r[v];
+  }
 }
 
 __device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
@@ -232,24 +239,27 @@ __device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
 }
 
 // Hash keys [first, first+nk) of kd into h[PER] (key r*NT+t -> thread t, h[r]).
-// `tile` is LDS scratch of K20Tile<NT>::kVec uint4 (K20 only).
+// `tile` is LDS scratch of K20Tile<NT, KPT>::kVec uint4 (K20 only).
+constexpr int kTileKPT = 2;  // keys per thread per LDS tile (20 KiB tiles at 512 threads)
+
 template <int MODE, int NT, int PER>
 __device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, uint32_t nk,
                                            uint4* tile, uint32_t (&h)[PER]) {
   const int t = threadIdx.x;
   if constexpr (MODE == KM_K20) {
-    constexpr int KPT = 4;
+    constexpr int KPT = kTileKPT;
+    using TL = K20Tile<NT, KPT>;
     constexpr int NTILES = PER / KPT;
     const uint8_t* base = kd.bytes + first * 20u;
     const uint32_t nbytes = nk * 20u;
-    uint4 pre[K20Tile<NT>::kPer];
-    k20_tile_fetch<NT>(base, nbytes, 0, pre);
+    uint4 pre[TL::kPer];
+    k20_tile_fetch<NT, KPT>(base, nbytes, 0, pre);
 #pragma unroll
     for (int q = 0; q < NTILES; q++) {
-      k20_tile_store<NT>(tile, pre);
+      k20_tile_store<NT, KPT>(tile, pre);
       __syncthreads();
-      if (q + 1 < NTILES && (q + 1) * K20Tile<NT>::kKeys < static_cast<int>(nk))
-        k20_tile_fetch<NT>(base, nbytes, q + 1, pre);
+      if (q + 1 < NTILES && (q + 1) * TL::kKeys < static_cast<int>(nk))
+        k20_tile_fetch<NT, KPT>(base, nbytes, q + 1, pre);
       const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
 #pragma unroll
       for (int j = 0; j < KPT; j++) {
@@ -324,7 +334,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     int lgR) {
   constexpr int C = kBuildChunk;
   constexpr int PER = C / kPartBlock;
-  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock>::kVec : 1];
+  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock, kTileKPT>::kVec : 1];
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
   __shared__ uint32_t wsum[kPartBlock / 64];
@@ -396,7 +406,9 @@ __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint
 // entries in flight per lane), ORs bits with ds_or, and the slice streams out
 // with 16-byte stores.
 // ---------------------------------------------------------------------------
-constexpr int kSliceBlock = 512;
+constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
+constexpr int kProbeSliceBlock = 1024;  // probe slices (64 KiB LDS -> 2 per CU, 32 waves)
+constexpr int kWalkU = 8;               // hashes in flight per lane in the segment walks
 
 template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
@@ -404,7 +416,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
     const uint32_t* __restrict__ tab) {
   constexpr uint32_t R = 1u << LGR;
-  constexpr int U = 4;
+  constexpr int U = kWalkU;
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
@@ -605,7 +617,9 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint32_t* __restrict__ tab) {
   constexpr int C = kProbeChunk;
   constexpr int PER = C / kPartBlock;
-  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock>::kVec : 1];
+  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock, kTileKPT>::kVec : 1];
+  __shared__ uint16_t rk[C];  // each key's rank inside its slice bucket
+  __shared__ uint8_t sb[C];   // each key's slice (S <= 256)
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint32_t wsum[kPartBlock / 64];
   const int tid = threadIdx.x;
@@ -616,13 +630,13 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
   for (uint32_t b = tid; b <= S; b += kPartBlock) hist[b] = 0;
   uint32_t h[PER];
   hash_chunk<MODE, kPartBlock, PER>(kd, first, nk, tile, h);  // ends with a barrier
-  uint32_t code[PER];
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
-      const uint32_t s = fastmod(h[r], L, magic) >> lgR;
-      code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
+      const uint32_t sl = fastmod(h[r], L, magic) >> lgR;
+      sb[i] = static_cast<uint8_t>(sl);
+      rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
     }
   }
   __syncthreads();
@@ -632,7 +646,7 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
-      const uint32_t p = hist[code[r] & 511u] + (code[r] >> 9);
+      const uint32_t p = hist[sb[i]] + rk[i];
       entries[first + p] = h[r];
       pos[first + i] = static_cast<uint16_t>(p);
     }
@@ -644,13 +658,13 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
 // chunks at a time with 4 hashes in flight per lane.  smask gets each key's
 // F-bit answer at the key's bucketed position.
 template <int LGR>
-__global__ __launch_bounds__(kSliceBlock) void probe_slice_kernel(
+__global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint32_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
-  constexpr int U = 4;
-  constexpr int NW = kSliceBlock / 64;
+  constexpr int U = kWalkU;
+  constexpr int NW = kProbeSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint64_t sl[R * 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t s = blockIdx.x % S;
@@ -660,7 +674,7 @@ __global__ __launch_bounds__(kSliceBlock) void probe_slice_kernel(
   {
     const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 64u);
     uint4* dst = reinterpret_cast<uint4*>(sl);
-    for (uint32_t w = tid; w < nl * 32u; w += kSliceBlock) dst[w] = src[w];
+    for (uint32_t w = tid; w < nl * 32u; w += kProbeSliceBlock) dst[w] = src[w];
   }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
@@ -910,7 +924,7 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
                                const uint32_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (lgR != 7) return hipErrorInvalidValue;
-  probe_slice_kernel<7><<<n_slices * parts, kSliceBlock, 0, s>>>(stacked, L, magic, k, n_slices,
+  probe_slice_kernel<7><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(stacked, L, magic, k, n_slices,
                                                                  n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
