@@ -260,7 +260,7 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
     return from_hip(e);
   }
   ctx->stream = ctx->own;
-  ctx->probe_round = 16ull << 20;
+  ctx->probe_round = 0;
   if (const char* e = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(e, nullptr, 10);
   *out = ctx;
   return DLSM_OK;
@@ -385,7 +385,7 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     d.bpk = bits_per_key;
     starts[j] = chunk;
     starts[n_jobs + j] = slice;
-    entry += b.keys.n;
+    entry += (b.keys.n + 15) & ~uint64_t(15);  // 16-element aligned: 16-byte stores
     chunk += d.n_chunks;
     slice += d.n_slices;
     tabw += static_cast<uint64_t>(d.n_slices + 1) * d.n_chunks;

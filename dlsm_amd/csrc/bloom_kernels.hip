@@ -320,6 +320,23 @@ __device__ __forceinline__ int wave_seg_find(uint32_t excl, uint32_t e) {
   return lo;
 }
 
+// Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
+// global base is 16-byte aligned: chunk starts are multiples of 4096 elements).
+template <int NT>
+__device__ __forceinline__ void store_chunk_u32(uint32_t* g, const uint32_t* lds, uint32_t n) {
+  const uint32_t nv = n / 4u;
+  for (uint32_t v = threadIdx.x; v < nv; v += NT)
+    reinterpret_cast<uint4*>(g)[v] = reinterpret_cast<const uint4*>(lds)[v];
+  for (uint32_t i = nv * 4u + threadIdx.x; i < n; i += NT) g[i] = lds[i];
+}
+template <int NT>
+__device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds, uint32_t n) {
+  const uint32_t nv = n / 8u;
+  for (uint32_t v = threadIdx.x; v < nv; v += NT)
+    reinterpret_cast<uint4*>(g)[v] = reinterpret_cast<const uint4*>(lds)[v];
+  for (uint32_t i = nv * 8u + threadIdx.x; i < n; i += NT) g[i] = lds[i];
+}
+
 // ---------------------------------------------------------------------------
 // Full filter build, pass 1: hash + consecutive-dedup count (+ slice
 // partition).  One 512-thread workgroup per chunk of kBuildChunk keys of one
@@ -334,7 +351,9 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     int lgR) {
   constexpr int C = kBuildChunk;
   constexpr int PER = C / kPartBlock;
-  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock, kTileKPT>::kVec : 1];
+  // key tile (K20), then the staging area of the bucketed hashes (both modes)
+  __shared__ __attribute__((aligned(16))) uint4 tile[K20Tile<kPartBlock, kTileKPT>::kVec];
+  static_assert(K20Tile<kPartBlock, kTileKPT>::kVec * 16 >= C * 4, "staging fits the tile");
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
   __shared__ uint32_t wsum[kPartBlock / 64];
@@ -372,12 +391,14 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
   for (uint32_t b = tid; b <= S; b += kPartBlock)
     tab[J.tab0 + static_cast<uint64_t>(b) * J.n_chunks + c] = hist[b];
-  uint32_t* ent = entries + J.entry0 + first;
+  uint32_t* stage = reinterpret_cast<uint32_t*>(tile);  // free since hash_chunk's last barrier
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
-    if (i < nk) ent[hist[code[r] & 511u] + (code[r] >> 9)] = h[r];
+    if (i < nk) stage[hist[code[r] & 511u] + (code[r] >> 9)] = h[r];
   }
+  __syncthreads();
+  store_chunk_u32<kPartBlock>(entries + J.entry0 + first, stage, nk);
 }
 
 // Sum of a job's per-chunk distinct counts (every thread gets the total).
@@ -617,9 +638,11 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint32_t* __restrict__ tab) {
   constexpr int C = kProbeChunk;
   constexpr int PER = C / kPartBlock;
-  __shared__ __attribute__((aligned(16))) uint4 tile[MODE == KM_K20 ? K20Tile<kPartBlock, kTileKPT>::kVec : 1];
-  __shared__ uint16_t rk[C];  // each key's rank inside its slice bucket
-  __shared__ uint8_t sb[C];   // each key's slice (S <= 256)
+  constexpr int TV = K20Tile<kPartBlock, kTileKPT>::kVec;
+  static_assert(TV * 16 >= C * 4, "the key tile doubles as the bucketed-hash staging area");
+  __shared__ __attribute__((aligned(16))) uint4 tile[TV];
+  __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
+  __shared__ uint8_t sb[C];                                // slice (S <= 256)
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint32_t wsum[kPartBlock / 64];
   const int tid = threadIdx.x;
@@ -642,15 +665,20 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
   __syncthreads();
   block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
   for (uint32_t b = tid; b <= S; b += kPartBlock) tab[static_cast<uint64_t>(b) * nC + c] = hist[b];
+  uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
       const uint32_t p = hist[sb[i]] + rk[i];
-      entries[first + p] = h[r];
-      pos[first + i] = static_cast<uint16_t>(p);
+      stage[p] = h[r];
+      rk[i] = static_cast<uint16_t>(p);
     }
   }
+  __syncthreads();
+  // coalesced 16-byte stores of the bucketed hashes and of the positions
+  store_chunk_u32<kPartBlock>(entries + first, stage, nk);
+  store_chunk_u16<kPartBlock>(pos + first, rk, nk);
 }
 
 // Pass 2: one 512-thread workgroup per (slice of 2^LGR stacked lines, part of
