@@ -623,8 +623,9 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   // per key) of one round stay resident in the 256 MiB Infinity Cache, and the
   // next round overwrites the same lines, so they never stream to HBM.
   const uint64_t n = keys->n;
-  uint64_t round = ctx->probe_round ? ctx->probe_round : n;
-  round = std::max<uint64_t>(kProbeChunk, (round / kProbeChunk) * kProbeChunk);
+  uint64_t round = n;
+  if (ctx->probe_round && ctx->probe_round < n)
+    round = std::max<uint64_t>(kProbeChunk, (ctx->probe_round / kProbeChunk) * kProbeChunk);
   const uint64_t rk = std::min(round, n);
   const uint32_t nCmax = ceil_div_u32(rk, kProbeChunk);
   DLSM_CHECK(ctx->entries.ensure(rk));

@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
             const int li = wave_seg_find(excl, ec);
             const uint64_t idx = static_cast<uint64_t>(g + li) * kBuildChunk +
                                  __shfl(o0, li, 64) + (ec - __shfl(excl, li, 64));
-            hv[u] = ok[u] ? ent[idx] : 0u;
+            hv[u] = ent[idx];  // idx is valid for every lane (clamped e): no select around the load
           }
 #pragma unroll
           for (int u = 0; u < U; u++)
@@ -685,7 +685,7 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
 // the chunks); the slice sits in LDS, waves walk the slice's segments of 64
 // chunks at a time with 4 hashes in flight per lane.  smask gets each key's
 // F-bit answer at the key's bucketed position.
-template <int LGR>
+template <int LGR, int K>
 __global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint32_t* __restrict__ tab,
@@ -728,7 +728,7 @@ __global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
         const int li = wave_seg_find(excl, ec);
         idx[u] = static_cast<uint64_t>(g + li) * kProbeChunk + __shfl(o0, li, 64) +
                  (ec - __shfl(excl, li, 64));
-        hv[u] = ok[u] ? entries[idx[u]] : 0u;
+        hv[u] = entries[idx[u]];  // valid for every lane (clamped e): no select around the load
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -737,10 +737,25 @@ __global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
         const uint64_t* ln = sl + (fastmod(x, L, magic) - lo_line) * 64u;
         const uint32_t delta = bloom_delta(x);
         uint64_t acc = 0x0101010101010101ull;
-        for (int q = 0; q < k; q++) {
-          const uint32_t bp = x & 511u;
-          acc &= ln[bp >> 3] >> (bp & 7u);
-          x += delta;
+        if constexpr (K > 0) {
+          // k known at compile time: all k LDS reads issue back to back
+          uint64_t v[K];
+          uint32_t sh[K];
+#pragma unroll
+          for (int q = 0; q < K; q++) {
+            const uint32_t bp = x & 511u;
+            v[q] = ln[bp >> 3];
+            sh[q] = bp & 7u;
+            x += delta;
+          }
+#pragma unroll
+          for (int q = 0; q < K; q++) acc &= v[q] >> sh[q];
+        } else {
+          for (int q = 0; q < k; q++) {
+            const uint32_t bp = x & 511u;
+            acc &= ln[bp >> 3] >> (bp & 7u);
+            x += delta;
+          }
         }
         acc &= 0x0101010101010101ull;
         smask[idx[u]] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
@@ -952,8 +967,12 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
                                const uint32_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (lgR != 7) return hipErrorInvalidValue;
-  probe_slice_kernel<7><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(stacked, L, magic, k, n_slices,
-                                                                 n_chunks, entries, tab, smask, parts);
+  if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
+    probe_slice_kernel<7, 6><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(
+        stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
+  else
+    probe_slice_kernel<7, 0><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(
+        stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
 
