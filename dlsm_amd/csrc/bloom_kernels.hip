@@ -308,16 +308,33 @@ __device__ __forceinline__ uint32_t chunk_distinct(const uint32_t (&h)[PER], uin
   return tot;
 }
 
-// Largest lane l whose exclusive prefix excl[l] <= e (excl non-decreasing
-// across the wave).  Every lane must be active.
-__device__ __forceinline__ int wave_seg_find(uint32_t excl, uint32_t e) {
-  int lo = 0;
-#pragma unroll
-  for (int step = 32; step > 0; step >>= 1) {
-    const uint32_t v = __shfl(excl, lo + step, 64);
-    if (v <= e) lo += step;
+// Segment walk over one group of up to 64 chunks.  Lane l holds segment l's
+// flat start `excl` (non-decreasing; empty and out-of-range segments repeat
+// the next start) and its offset `off` inside chunk l's region.  For the batch
+// of flat entries [b0, b0+64) (b0 uniform) each lane finds the segment holding
+// its entry min(b0+lane, T-1).  `sc` (uniform) carries the segment of the batch
+// start from batch to batch.  Only v_readlane + compares: the ~4 segment
+// boundaries inside a batch cost a few VALU ops, no LDS round trips.
+__device__ __forceinline__ void seg_locate(uint32_t excl, uint32_t off, uint32_t T, uint32_t b0,
+                                           uint32_t& sc, uint32_t& li, uint32_t& st,
+                                           uint32_t& of) {
+  while (sc + 1 < 64 && static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, sc + 1)) <= b0) sc++;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t e = min(b0 + lane, T - 1u);
+  const uint32_t last = min(b0 + 63u, T - 1u);
+  li = sc;
+  st = static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, sc));
+  of = static_cast<uint32_t>(__builtin_amdgcn_readlane(off, sc));
+  for (uint32_t j = sc + 1; j < 64; j++) {
+    const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, j));
+    if (bj > last) break;
+    const uint32_t oj = static_cast<uint32_t>(__builtin_amdgcn_readlane(off, j));
+    if (e >= bj) {
+      li = j;
+      st = bj;
+      of = oj;
+    }
   }
-  return lo;
 }
 
 // Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
@@ -471,18 +488,19 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t excl = incl - cnt;
         const uint32_t T = __shfl(incl, 63, 64);
+        uint32_t sc = 0;
         for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
           uint32_t hv[U];
           bool ok[U];
 #pragma unroll
           for (int u = 0; u < U; u++) {
-            const uint32_t e = e0 + u * 64u + lane;
-            ok[u] = e < T;
-            const uint32_t ec = ok[u] ? e : T - 1u;
-            const int li = wave_seg_find(excl, ec);
-            const uint64_t idx = static_cast<uint64_t>(g + li) * kBuildChunk +
-                                 __shfl(o0, li, 64) + (ec - __shfl(excl, li, 64));
-            hv[u] = ent[idx];  // idx is valid for every lane (clamped e): no select around the load
+            const uint32_t b0 = e0 + u * 64u;
+            ok[u] = b0 + lane < T;
+            uint32_t li = 0, st = 0, of = 0;
+            if (b0 < T) seg_locate(excl, o0, T, b0, sc, li, st, of);
+            const uint32_t ec = min(b0 + lane, T - 1u);
+            const uint64_t idx = static_cast<uint64_t>(g + li) * kBuildChunk + of + (ec - st);
+            hv[u] = ent[idx];  // valid for every lane (clamped e): no select around the load
           }
 #pragma unroll
           for (int u = 0; u < U; u++)
@@ -686,7 +704,7 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
 // chunks at a time with 4 hashes in flight per lane.  smask gets each key's
 // F-bit answer at the key's bucketed position.
 template <int LGR, int K>
-__global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
+__global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint32_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
@@ -700,9 +718,20 @@ __global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
   const uint32_t lo_line = s << LGR;
   const uint32_t nl = min(R, L - lo_line);
   {
+    // all of the slice's 16-byte loads in flight before the first LDS store
+    constexpr int V = R * 32 / kProbeSliceBlock;
     const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 64u);
     uint4* dst = reinterpret_cast<uint4*>(sl);
-    for (uint32_t w = tid; w < nl * 32u; w += kProbeSliceBlock) dst[w] = src[w];
+    const uint32_t nw = nl * 32u;
+    uint4 t0 = src[min(static_cast<uint32_t>(0 * kProbeSliceBlock + tid), nw - 1u)];
+    uint4 t1 = src[min(static_cast<uint32_t>(1 * kProbeSliceBlock + tid), nw - 1u)];
+    uint4 t2 = src[min(static_cast<uint32_t>(2 * kProbeSliceBlock + tid), nw - 1u)];
+    uint4 t3 = src[min(static_cast<uint32_t>(3 * kProbeSliceBlock + tid), nw - 1u)];
+    static_assert(V == 4, "prologue written for 4 x 16 B per thread");
+    if (0 * kProbeSliceBlock + tid < nw) dst[0 * kProbeSliceBlock + tid] = t0;
+    if (1 * kProbeSliceBlock + tid < nw) dst[1 * kProbeSliceBlock + tid] = t1;
+    if (2 * kProbeSliceBlock + tid < nw) dst[2 * kProbeSliceBlock + tid] = t2;
+    if (3 * kProbeSliceBlock + tid < nw) dst[3 * kProbeSliceBlock + tid] = t3;
   }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
@@ -716,18 +745,19 @@ __global__ __launch_bounds__(kProbeSliceBlock) void probe_slice_kernel(
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t excl = incl - cnt;
     const uint32_t T = __shfl(incl, 63, 64);
+    uint32_t sc = 0;
     for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
       uint32_t hv[U];
       uint64_t idx[U];
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const uint32_t e = e0 + u * 64u + lane;
-        ok[u] = e < T;
-        const uint32_t ec = ok[u] ? e : T - 1u;
-        const int li = wave_seg_find(excl, ec);
-        idx[u] = static_cast<uint64_t>(g + li) * kProbeChunk + __shfl(o0, li, 64) +
-                 (ec - __shfl(excl, li, 64));
+        const uint32_t b0 = e0 + u * 64u;
+        ok[u] = b0 + lane < T;
+        uint32_t li = 0, st = 0, of = 0;
+        if (b0 < T) seg_locate(excl, o0, T, b0, sc, li, st, of);
+        const uint32_t ec = min(b0 + lane, T - 1u);
+        idx[u] = static_cast<uint64_t>(g + li) * kProbeChunk + of + (ec - st);
         hv[u] = entries[idx[u]];  // valid for every lane (clamped e): no select around the load
       }
 #pragma unroll
