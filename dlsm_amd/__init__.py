@@ -27,6 +27,7 @@ __all__ = [
     "Keys", "Context", "FilterSet", "DlsmError", "device_available", "bloom_hash",
     "full_size", "legacy_size", "full_parse", "FullFilterBlockBuilder",
     "FullFilterBlockReader", "BloomFilterPolicy", "PATH_AUTO", "PATH_DIRECT", "PATH_SLICED",
+    "crc32c", "crc32c_mask",
 ]
 
 PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
@@ -70,6 +71,16 @@ def full_parse(filt: bytes):
     k, L, lg = C.c_int(0), C.c_uint32(0), C.c_int(0)
     st = lib().dlsm_bloom_full_parse(b, len(filt), C.byref(k), C.byref(L), C.byref(lg))
     return st, k.value, L.value, lg.value
+
+
+def crc32c(data: bytes, init: int = 0) -> int:
+    """crc32c::Extend(init, data) (util/crc32c.h:17-22), host helper."""
+    b = C.create_string_buffer(bytes(data), len(data) + 1)
+    return int(lib().dlsm_crc32c_extend(init, b, len(data)))
+
+
+def crc32c_mask(crc: int) -> int:
+    return int(lib().dlsm_crc32c_mask(crc))
 
 
 def _ptr(x) -> Optional[int]:
@@ -211,6 +222,32 @@ class Context:
         jobs = self._jobs(tables, outs, caps)
         check(lib().dlsm_bloom_full_build_dev(self.h, jobs, len(tables), bits_per_key,
                                               _ptr(out_lens)), "full_build_dev")
+
+    def full_build_block(self, tables: Sequence[Keys], bits_per_key: int = 10, caps=None) -> list:
+        """Filter + 5-byte block trailer (FinishFilterBlock), host in/out."""
+        n = len(tables)
+        if caps is None:
+            caps = [full_size(t.n, bits_per_key)[0] + 5 for t in tables]
+        outs = [np.zeros(max(c, 1), dtype=np.uint8) for c in caps]
+        jobs = self._jobs(tables, outs, caps)
+        lens = (C.c_uint64 * max(n, 1))()
+        check(lib().dlsm_bloom_full_build_block(self.h, jobs, n, bits_per_key, lens), "full_build_block")
+        return [outs[j][: lens[j]].tobytes() for j in range(n)]
+
+    def full_build_block_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
+        caps = [int(o.numel()) for o in outs]
+        jobs = self._jobs(tables, outs, caps)
+        check(lib().dlsm_bloom_full_build_block_dev(self.h, jobs, len(tables), bits_per_key,
+                                                    _ptr(out_lens)), "full_build_block_dev")
+
+    def crc32c_dev(self, bufs) -> list:
+        """crc32c::Value of device tensors (uint8), computed on the GPU."""
+        n = len(bufs)
+        ptrs = (C.c_void_p * max(n, 1))(*[_ptr(b) for b in bufs])
+        lens = (C.c_uint64 * max(n, 1))(*[int(b.numel()) for b in bufs])
+        out = (C.c_uint32 * max(n, 1))()
+        check(lib().dlsm_crc32c_dev(self.h, ptrs, lens, n, out), "crc32c_dev")
+        return [int(out[j]) for j in range(n)]
 
     # -- full filter probe --------------------------------------------------
     def filterset(self, filters, on_device: bool = False) -> FilterSet:

@@ -60,6 +60,11 @@ SIGNATURES = [
     ("dlsm_host_unregister", C.c_int, [_VP]),
     ("dlsm_bloom_full_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
+    ("dlsm_bloom_full_build_block_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
+    ("dlsm_bloom_full_build_block", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
+    ("dlsm_crc32c_dev", C.c_int, [_VP, C.POINTER(_VP), _U64P, C.c_int, C.POINTER(C.c_uint32)]),
+    ("dlsm_crc32c_extend", C.c_uint32, [C.c_uint32, _VP, C.c_size_t]),
+    ("dlsm_crc32c_mask", C.c_uint32, [C.c_uint32]),
     ("dlsm_filterset_create", C.c_int, [_VP, C.POINTER(_VP), _U64P, C.c_int, C.c_int,
                                         C.POINTER(_VP)]),
     ("dlsm_filterset_destroy", C.c_int, [_VP]),

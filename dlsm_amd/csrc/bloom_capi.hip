@@ -77,7 +77,7 @@ struct dlsm_ctx {
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   // build workspace
   DevBuf<uint32_t> entries;
-  DevBuf<uint32_t> tab;
+  DevBuf<uint16_t> tab;  // chunk-major bucket offsets
   DevBuf<FullJobDev> jobs;
   DevBuf<uint32_t> starts;  // chunk0s | slice0s
   DevBuf<uint32_t> dchunk;  // per-chunk consecutive-distinct counts
@@ -96,6 +96,12 @@ struct dlsm_ctx {
   DevBuf<uint8_t> st_out;
   DevBuf<uint64_t> st_len;
   DevBuf<uint8_t> st_filter;
+  // crc32c / block sealing
+  DevBuf<uint8_t> crc_streams;
+  DevBuf<uint32_t> crc_partial;
+  DevBuf<uint8_t*> crc_outp;
+  DevBuf<uint64_t> crc_cap;
+  DevBuf<uint32_t> crc_val;
 };
 
 struct dlsm_filterset {
@@ -285,6 +291,11 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->st_out.release();
   ctx->st_len.release();
   ctx->st_filter.release();
+  ctx->crc_streams.release();
+  ctx->crc_partial.release();
+  ctx->crc_outp.release();
+  ctx->crc_cap.release();
+  ctx->crc_val.release();
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return DLSM_OK;
@@ -507,6 +518,140 @@ int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
   }
   DLSM_TRY(hipStreamSynchronize(s));
   return st;
+}
+
+// ---------------------------------------------------------------------------
+// Filter blocks (build + crc32c trailer) and crc32c of device buffers
+// ---------------------------------------------------------------------------
+uint32_t dlsm_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0x82f63b78u : (c >> 1);
+      table[i] = c;
+    }
+    init = true;
+  }
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  uint32_t c = ~init_crc;
+  for (size_t i = 0; i < n; i++) c = table[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+  return ~c;
+}
+
+uint32_t dlsm_crc32c_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+
+namespace {
+int run_crc(dlsm_ctx* ctx, const std::vector<std::vector<uint8_t>>& streams, int n, uint64_t max_total,
+            uint8_t* const* seal_out_host, const uint64_t* seal_cap_host, uint64_t* seal_len_dev,
+            uint32_t* crc_val_dev) {
+  hipStream_t s = ctx->stream;
+  const size_t ss = crc_stream_size();
+  const int max_parts = static_cast<int>(std::max<uint64_t>(1, crc_max_parts(max_total)));
+  DLSM_CHECK(ctx->crc_streams.ensure(ss * n));
+  DLSM_CHECK(ctx->crc_partial.ensure(static_cast<size_t>(max_parts) * n));
+  std::vector<uint8_t> flat(ss * n);
+  for (int j = 0; j < n; j++) memcpy(flat.data() + ss * j, streams[j].data(), ss);
+  DLSM_TRY(hipMemcpyAsync(ctx->crc_streams.p, flat.data(), ss * n, hipMemcpyHostToDevice, s));
+  uint8_t* const* seal_out = nullptr;
+  const uint64_t* seal_cap = nullptr;
+  if (seal_out_host) {
+    DLSM_CHECK(ctx->crc_outp.ensure(n));
+    DLSM_CHECK(ctx->crc_cap.ensure(n));
+    DLSM_TRY(hipMemcpyAsync(ctx->crc_outp.p, seal_out_host, sizeof(uint8_t*) * n, hipMemcpyHostToDevice, s));
+    DLSM_TRY(hipMemcpyAsync(ctx->crc_cap.p, seal_cap_host, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    seal_out = ctx->crc_outp.p;
+    seal_cap = ctx->crc_cap.p;
+  }
+  DLSM_TRY(launch_crc_streams(ctx->crc_streams.p, n, max_parts, ctx->crc_partial.p, seal_out, seal_cap,
+                              seal_len_dev, crc_val_dev, s));
+  return DLSM_OK;
+}
+}  // namespace
+
+int dlsm_bloom_full_build_block_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                    int bits_per_key, uint64_t* out_len_dev) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  // The filter must leave room for the 5-byte trailer.
+  std::vector<dlsm_build_job> fj(jobs, jobs + n_jobs);
+  std::vector<uint8_t*> outs(n_jobs);
+  std::vector<uint64_t> caps(n_jobs);
+  uint64_t max_total = 0;
+  for (int j = 0; j < n_jobs; j++) {
+    fj[j].out_cap = jobs[j].out_cap >= 5 ? jobs[j].out_cap - 5 : 0;
+    outs[j] = jobs[j].out;
+    caps[j] = jobs[j].out_cap;
+    max_total = std::max(max_total, full_filter_len(jobs[j].keys.n, bits_per_key) + 1);
+  }
+  DLSM_CHECK(dlsm_bloom_full_build_dev(ctx, fj.data(), n_jobs, bits_per_key, out_len_dev));
+  std::vector<std::vector<uint8_t>> st(n_jobs, std::vector<uint8_t>(crc_stream_size()));
+  for (int j = 0; j < n_jobs; j++) crc_stream_fill(st[j].data(), jobs[j].out, out_len_dev + j, 0, 1);
+  return run_crc(ctx, st, n_jobs, max_total, outs.data(), caps.data(), out_len_dev, nullptr);
+}
+
+int dlsm_bloom_full_build_block(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                int bits_per_key, uint64_t* out_len) {
+  if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
+  if (n_jobs == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  std::vector<const dlsm_keyset*> sets(n_jobs);
+  for (int j = 0; j < n_jobs; j++) {
+    DLSM_CHECK(validate_keyset(jobs[j].keys));
+    if (!jobs[j].out) return DLSM_E_ARG;
+    sets[j] = &jobs[j].keys;
+  }
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets.data(), n_jobs, dk));
+  std::vector<dlsm_build_job> dj(n_jobs);
+  std::vector<uint64_t> opos(n_jobs);
+  uint64_t obytes = 0;
+  for (int j = 0; j < n_jobs; j++) {
+    const uint64_t spec = full_filter_len(jobs[j].keys.n, bits_per_key) + 5;
+    const uint64_t cap = std::min(spec, jobs[j].out_cap);
+    opos[j] = obytes;
+    obytes += (cap + 255) & ~uint64_t(255);
+    dj[j].keys = dk[j];
+    dj[j].out_cap = cap;
+  }
+  DLSM_CHECK(ctx->st_out.ensure(obytes + 256));
+  DLSM_CHECK(ctx->st_len.ensure(n_jobs));
+  for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
+  DLSM_CHECK(dlsm_bloom_full_build_block_dev(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p));
+  hipStream_t s = ctx->stream;
+  DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
+  DLSM_TRY(hipStreamSynchronize(s));
+  int st = DLSM_OK;
+  for (int j = 0; j < n_jobs; j++) {
+    if (out_len[j] == 0) {
+      st = DLSM_E_CAPACITY;
+      continue;
+    }
+    DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
+  }
+  DLSM_TRY(hipStreamSynchronize(s));
+  return st;
+}
+
+int dlsm_crc32c_dev(dlsm_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, int n,
+                    uint32_t* crc_out) {
+  if (!ctx || n < 0 || (n > 0 && (!bufs || !lens || !crc_out))) return DLSM_E_ARG;
+  if (n == 0) return DLSM_OK;
+  DeviceGuard g(ctx->device);
+  std::vector<std::vector<uint8_t>> st(n, std::vector<uint8_t>(crc_stream_size()));
+  uint64_t max_total = 0;
+  for (int j = 0; j < n; j++) {
+    if (lens[j] && !bufs[j]) return DLSM_E_ARG;
+    crc_stream_fill(st[j].data(), bufs[j], nullptr, lens[j], 0);
+    max_total = std::max(max_total, lens[j]);
+  }
+  DLSM_CHECK(ctx->crc_val.ensure(n));
+  DLSM_CHECK(run_crc(ctx, st, n, max_total, nullptr, nullptr, nullptr, ctx->crc_val.p));
+  DLSM_TRY(hipMemcpyAsync(crc_out, ctx->crc_val.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  return DLSM_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -29,7 +29,7 @@ struct FullJobDev {
   uint64_t out_cap;
   uint64_t* out_len;   // device slot for this job's length
   uint64_t entry0;     // first entry of this job in the entry workspace
-  uint64_t tab0;       // first word of this job's (n_slices+1) x n_chunks table
+  uint64_t tab0;       // first u16 of this job's n_chunks x (n_slices+1) bucket-offset table
   uint32_t chunk0, n_chunks;
   uint32_t slice0, n_slices;
   uint32_t L_spec, magic_spec;  // speculative line count (no duplicates) + fastmod magic
@@ -71,10 +71,10 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
                                uint32_t total_chunks, const uint32_t* jobL, int mode, hipStream_t s);
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                  uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
-                                 uint32_t* tab, int lgR, int mode, hipStream_t s);
+                                 uint16_t* tab, int lgR, int mode, hipStream_t s);
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t total_slices, const uint32_t* dchunk,
-                              const uint32_t* entries, const uint32_t* tab, int lgR, hipStream_t s);
+                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s);
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
                                int mode, hipStream_t s);
@@ -82,10 +82,10 @@ hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, 
                                 hipStream_t s);
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint32_t* tab, int mode, hipStream_t s);
+                                  uint16_t* tab, int mode, hipStream_t s);
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
                                int lgR, uint32_t n_slices, uint32_t n_chunks,
-                               const uint32_t* entries, const uint32_t* tab, uint8_t* smask,
+                               const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
                                int parts, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                   uint8_t* mask, hipStream_t s);
@@ -94,5 +94,14 @@ hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,
                                int trivial, KeyDesc keys, uint8_t* out, int mode, hipStream_t s);
+
+// block_crc.hip: crc32c of device streams, optionally sealing filter blocks.
+uint64_t crc_max_parts(uint64_t max_len_plus_extra);
+size_t crc_stream_size();
+void crc_stream_fill(void* dst, const uint8_t* data, const uint64_t* len_dev, uint64_t len_host,
+                     uint32_t extra);
+hipError_t launch_crc_streams(const void* streams, int n, int max_parts, uint32_t* partial,
+                              uint8_t* const* seal_out, const uint64_t* seal_cap, uint64_t* seal_len,
+                              uint32_t* crc_out, hipStream_t s);
 
 }  // namespace dlsm

@@ -364,7 +364,7 @@ constexpr int kPartBlock = 512;
 template <int MODE, bool PART>
 __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
-    uint32_t* __restrict__ dchunk, uint32_t* __restrict__ entries, uint32_t* __restrict__ tab,
+    uint32_t* __restrict__ dchunk, uint32_t* __restrict__ entries, uint16_t* __restrict__ tab,
     int lgR) {
   constexpr int C = kBuildChunk;
   constexpr int PER = C / kPartBlock;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   __syncthreads();
   block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
   for (uint32_t b = tid; b <= S; b += kPartBlock)
-    tab[J.tab0 + static_cast<uint64_t>(b) * J.n_chunks + c] = hist[b];
+    tab[J.tab0 + static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);  // free since hash_chunk's last barrier
 #pragma unroll
   for (int r = 0; r < PER; r++) {
@@ -452,7 +452,7 @@ template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ slice0s, int n_jobs,
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
-    const uint32_t* __restrict__ tab) {
+    const uint16_t* __restrict__ tab) {
   constexpr uint32_t R = 1u << LGR;
   constexpr int U = kWalkU;
   constexpr int NW = kSliceBlock / 64;
@@ -478,13 +478,13 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const uint32_t magic = fastmod_magic(L);
     if (L == J.L_spec) {
       const uint32_t nC = J.n_chunks;
-      const uint32_t* row0 = tab + J.tab0 + static_cast<uint64_t>(s) * nC;
-      const uint32_t* row1 = row0 + nC;
+      const uint16_t* tb = tab + J.tab0 + s;  // chunk-major rows of n_slices+1 u16
       const uint32_t* ent = entries + J.entry0;
       for (uint32_t g = wv * 64u; g < nC; g += NW * 64u) {
         const uint32_t c = g + lane;
-        const uint32_t o0 = c < nC ? row0[c] : 0u;
-        const uint32_t cnt = c < nC ? row1[c] - o0 : 0u;
+        const uint16_t* r = tb + static_cast<uint64_t>(c) * (J.n_slices + 1);
+        const uint32_t o0 = c < nC ? r[0] : 0u;
+        const uint32_t cnt = c < nC ? r[1] - o0 : 0u;
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t excl = incl - cnt;
         const uint32_t T = __shfl(incl, 63, 64);
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
 template <int MODE>
 __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
-    uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint32_t* __restrict__ tab) {
+    uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
   constexpr int C = kProbeChunk;
   constexpr int PER = C / kPartBlock;
   constexpr int TV = K20Tile<kPartBlock, kTileKPT>::kVec;
@@ -682,7 +682,8 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
   }
   __syncthreads();
   block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
-  for (uint32_t b = tid; b <= S; b += kPartBlock) tab[static_cast<uint64_t>(b) * nC + c] = hist[b];
+  for (uint32_t b = tid; b <= S; b += kPartBlock)
+    tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);  // one row per chunk
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
   for (int r = 0; r < PER; r++) {
@@ -706,7 +707,7 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
 template <int LGR, int K>
 __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
-    uint32_t nC, const uint32_t* __restrict__ entries, const uint32_t* __restrict__ tab,
+    uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
   constexpr int U = kWalkU;
@@ -735,13 +736,13 @@ __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
   }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
-  const uint32_t* row0 = tab + static_cast<uint64_t>(s) * nC;
-  const uint32_t* row1 = row0 + nC;
+  const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
   __syncthreads();
   for (uint32_t g = c_lo + wv * 64u; g < c_hi; g += NW * 64u) {
     const uint32_t c = g + lane;
-    const uint32_t o0 = c < c_hi ? row0[c] : 0u;
-    const uint32_t cnt = c < c_hi ? row1[c] - o0 : 0u;
+    const uint16_t* r = tb + static_cast<uint64_t>(c) * (S + 1);
+    const uint32_t o0 = c < c_hi ? r[0] : 0u;
+    const uint32_t cnt = c < c_hi ? r[1] - o0 : 0u;
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t excl = incl - cnt;
     const uint32_t T = __shfl(incl, 63, 64);
@@ -929,7 +930,7 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
 
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                  uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
-                                 uint32_t* tab, int lgR, int mode, hipStream_t s) {
+                                 uint16_t* tab, int lgR, int mode, hipStream_t s) {
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
     full_partition_kernel<KM_K20, true><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
@@ -942,7 +943,7 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
 
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t total_slices, const uint32_t* dchunk,
-                              const uint32_t* entries, const uint32_t* tab, int lgR, hipStream_t s) {
+                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s) {
   if (total_slices == 0) return hipSuccess;
   switch (lgR) {
     case 9:
@@ -980,7 +981,7 @@ hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, 
 
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint32_t* tab, int mode, hipStream_t s) {
+                                  uint16_t* tab, int mode, hipStream_t s) {
   const uint32_t nC = static_cast<uint32_t>((keys.n + kProbeChunk - 1) / kProbeChunk);
   if (nC == 0) return hipSuccess;
   if (mode == KM_K20)
@@ -994,7 +995,7 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
 
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR,
                                uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
-                               const uint32_t* tab, uint8_t* smask, int parts, hipStream_t s) {
+                               const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (lgR != 7) return hipErrorInvalidValue;
   if (k == 6)  // bits_per_key 10 (ChooseNumProbes)

@@ -66,7 +66,7 @@ typedef struct {
 /* One SSTable's filter: its keys in table order and its output slot. */
 typedef struct {
   dlsm_keyset keys;
-  uint8_t* out;     /* output slot (4-byte aligned) */
+  uint8_t* out;     /* output slot (16-byte aligned for the _dev calls) */
   uint64_t out_cap; /* slot capacity in bytes */
 } dlsm_build_job;
 
@@ -135,6 +135,24 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
  * small (its out_len is 0). */
 int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
                           int bits_per_key, uint64_t* out_len);
+
+/* FinishFilterBlock (table/table_builder_computeside.cc:389-432): the full
+ * filter followed by the 5-byte block trailer [type 0][Fixed32(crc32c::Mask(
+ * crc32c(filter || type)))] -- the exact bytes FlushFilter RDMA-writes
+ * (:551-567).  out_len = filter length + 5, or 0 if the slot is too small.
+ * crc32c on the GPU (util/crc32c.h:17-37 semantics). */
+int dlsm_bloom_full_build_block_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                    int bits_per_key, uint64_t* out_len_dev);
+int dlsm_bloom_full_build_block(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                int bits_per_key, uint64_t* out_len);
+
+/* crc32c::Value of n device buffers on the GPU (ReadFilterBlock's check,
+ * table/format.cc:398-408); crc_out: host uint32[n].  Synchronous. */
+int dlsm_crc32c_dev(dlsm_ctx* ctx, const uint8_t* const* bufs, const uint64_t* lens, int n,
+                    uint32_t* crc_out);
+/* Host helpers: crc32c::Extend and crc32c::Mask (util/crc32c.h:17-31). */
+uint32_t dlsm_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
+uint32_t dlsm_crc32c_mask(uint32_t crc);
 
 /* ---- full filter, probe ------------------------------------------------- */
 

@@ -102,6 +102,10 @@ def ref_lib():
         R.ref_full_build.restype = C.c_int64
         R.ref_full_build.argtypes = [cp, u64p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
         R.ref_full_may_match.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
+        R.ref_crc32c_extend.restype = C.c_uint32
+        R.ref_crc32c_extend.argtypes = [C.c_uint32, cp, C.c_size_t]
+        R.ref_crc32c_mask.restype = C.c_uint32
+        R.ref_crc32c_mask.argtypes = [C.c_uint32]
         _REF = R
     return _REF
 
@@ -239,6 +243,14 @@ def crc32c(data: bytes, init: int = 0) -> int:
 
 def crc32c_mask(crc: int) -> int:
     return int(lib().orc_crc32c_mask(crc))
+
+
+def filter_block(filt: bytes) -> bytes:
+    """The bytes FlushFilter RDMA-writes: filter + [type 0] + Fixed32(Mask(crc32c(filter||type)))
+    (table/table_builder_computeside.cc:418-428)."""
+    crc = crc32c(b"\0", crc32c(filt))
+    m = crc32c_mask(crc)
+    return filt + b"\0" + m.to_bytes(4, "little")
 
 
 def full_build_many(tables: list[np.ndarray], ns: list[int], stride: int, bpk: int,

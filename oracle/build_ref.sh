@@ -15,5 +15,6 @@ mkdir -p "$OUT"
 g++ -std=c++17 -O2 -DNDEBUG -DHAVE_SNAPPY=0 -DTimberSaw_PLATFORM_POSIX=1 -fPIC -shared \
   -I"$REF" -I"$REF/include" \
   "$HERE/ref_driver.cc" "$REF/util/hash.cc" "$REF/util/bloom.cc" "$REF/util/filter_policy.cc" \
+  "$REF/util/crc32c.cc" \
   -o "$OUT/libref.so"
 echo "build_ref: built $OUT/libref.so"

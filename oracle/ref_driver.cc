@@ -8,6 +8,7 @@
 //   util/bloom.cc           BloomFilterPolicy CreateFilter / KeyMayMatch
 //   util/filter_policy.cc   ~FilterPolicy
 //   util/bloom_impl.h       LegacyLocalityBloomImpl<false>, ChooseNumProbes
+//   util/crc32c.cc          crc32c::Extend / Value / Mask (filter-block trailer)
 // table/full_filter_block.cc itself is NOT buildable here without a stand-in
 // <infiniband/verbs.h> (its include chain reaches util/rdma.h), which the task
 // rules forbid.  ref_full_build() therefore restates only its ~20 lines of
@@ -21,6 +22,7 @@
 #include "TimberSaw/filter_policy.h"
 #include "TimberSaw/slice.h"
 #include "util/bloom_impl.h"
+#include "util/crc32c.h"
 #include "util/hash.h"
 
 using TimberSaw::Slice;
@@ -108,5 +110,11 @@ int ref_full_may_match(const char* key, size_t klen, const char* filter, size_t 
   LegacyBloom::PrepareHashMayMatch(h, L, filter, &off, 6);
   return LegacyBloom::HashMayMatchPrepared(h, k, filter + off, 6) ? 1 : 0;
 }
+
+uint32_t ref_crc32c_extend(uint32_t init, const char* data, size_t n) {
+  return TimberSaw::crc32c::Extend(init, data, n);
+}
+
+uint32_t ref_crc32c_mask(uint32_t crc) { return TimberSaw::crc32c::Mask(crc); }
 
 }  // extern "C"

@@ -162,9 +162,30 @@ def main():
         f = ref_full(keys)
         digests.append({"name": f"config4_table{s}_{n}", "first": s, "step": 16, "n": n, "bpk": 10,
                         "len": len(f), "fnv1a64": oracle.fnv1a64(f)})
+    # filter blocks as FinishFilterBlock writes them (table_builder_computeside.cc:418-428):
+    # filter + [type 0] + Fixed32(crc32c::Mask(crc32c::Extend(Value(filter), type)))
+    blocks = []
+    for c in full:
+        if c["bpk"] != 10:
+            continue
+        fb = bytes.fromhex(c["filter"])
+        crc = R().ref_crc32c_extend(R().ref_crc32c_extend(0, fb, len(fb)), b"\0", 1)
+        blocks.append({"name": c["name"], "trailer": (b"\0" + R().ref_crc32c_mask(crc).to_bytes(4, "little")).hex()})
+    for d in digests:
+        if d.get("format") == "legacy":
+            continue
+        keys_np = oracle.dbbench_keys(d["first"], d["step"], d["n"]).tobytes()
+        fb = ref_full([keys_np[i * 20:(i + 1) * 20] for i in range(d["n"])])
+        crc = R().ref_crc32c_extend(R().ref_crc32c_extend(0, fb, len(fb)), b"\0", 1)
+        d["block_trailer"] = (b"\0" + R().ref_crc32c_mask(crc).to_bytes(4, "little")).hex()
+    crc_kats = []
+    for data in [bytes(32), b"\xff" * 32, bytes(range(32)), bytes(range(31, -1, -1)), b"hello world", b"",
+                 bytes([0x01, 0xc0] + [0] * 14 + [0x14, 0, 0, 0, 0, 0, 4, 0, 0, 0, 0, 0x14, 0, 0, 0, 0x18,
+                                               0x28] + [0] * 7 + [2] + [0] * 7)]:
+        crc_kats.append({"data": data.hex(), "crc": R().ref_crc32c_extend(0, data, len(data))})
     with open(os.path.join(HERE, "full.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py (reference bloom_impl.h AddHash)",
-                   "cases": full, "digests": digests}, f, indent=0)
+        json.dump({"generator": "tests/golden/make_golden.py (reference bloom_impl.h AddHash, crc32c.cc)",
+                   "cases": full, "digests": digests, "blocks": blocks, "crc32c": crc_kats}, f, indent=0)
 
     # ---------------- legacy (util/bloom.cc) ----------------
     leg = []

@@ -390,3 +390,65 @@ def test_full_size_properties(gpu, orc):
     single = gpu.filterset([filters[3]])
     m3 = gpu.full_probe(single, absent)
     assert np.array_equal(m3 & 1, (m >> 3) & 1)
+
+
+# ---------------------------------------------------------------------------
+# filter blocks (FinishFilterBlock trailer) and crc32c on the GPU
+# ---------------------------------------------------------------------------
+
+def test_filter_block_golden(gpu, golden, orc):
+    names = {c["name"]: c for c in golden["full"]["cases"]}
+    for b in golden["full"]["blocks"]:
+        c = names[b["name"]]
+        got = gpu.full_build_block([keys_of(c)], 10)[0]
+        assert got.hex() == c["filter"] + b["trailer"], b["name"]
+
+
+def test_filter_block_batch_vs_oracle(gpu, golden, orc):
+    import torch
+
+    import dlsm_amd
+
+    specs = [(s, 16, 153_846) for s in range(16)] + [(0, 1, 1_600_000), (3, 7, 1), (5, 3, 0)]
+    tables, outs, want = [], [], []
+    for first, step, n in specs:
+        k = orc.dbbench_keys(first, step, n) if n else np.zeros(16, np.uint8)
+        want.append(orc.filter_block(orc.full_build(k, n)))
+        tables.append(dlsm_amd.Keys(torch.from_numpy(k).cuda(), n, 20))
+        outs.append(torch.full((dlsm_amd.full_size(n)[0] + 5,), 0xEE, dtype=torch.uint8, device="cuda"))
+    lens = torch.zeros(len(specs), dtype=torch.uint64, device="cuda")
+    gpu.full_build_block_dev(tables, outs, lens, 10)
+    gpu.sync()
+    L = lens.cpu().numpy()
+    for j, w in enumerate(want):
+        assert int(L[j]) == len(w)
+        assert outs[j][: int(L[j])].cpu().numpy().tobytes() == w, specs[j]
+    d = [x for x in golden["full"]["digests"] if x["name"] == "dbbench_seq_1600000"][0]
+    assert want[16][-5:].hex() == d["block_trailer"]
+
+
+def test_filter_block_capacity(gpu, orc):
+    import dlsm_amd
+
+    k = orc.dbbench_keys(0, 1, 1000)
+    need = dlsm_amd.full_size(1000)[0] + 5
+    with pytest.raises(dlsm_amd.DlsmError) as e:
+        gpu.full_build_block([dlsm_amd.Keys(k, 1000, 20)], 10, caps=[need - 1])
+    assert e.value.status == -2
+
+
+def test_crc32c_dev_vs_oracle(gpu, golden, orc):
+    import torch
+
+    rng = np.random.default_rng(42)
+    bufs, want = [], []
+    for c in golden["full"]["crc32c"]:
+        b = bytes.fromhex(c["data"])
+        bufs.append(torch.tensor(list(b), dtype=torch.uint8, device="cuda"))
+        want.append(c["crc"])
+    for n in [1, 15, 16, 17, 1023, 1024, 16384, 65535, 65536, 65537, 2_000_069, 3_000_001]:
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        t = torch.from_numpy(b).cuda()
+        bufs.append(t[1:] if n > 100 else t)  # also an unaligned start
+        want.append(orc.crc32c((b[1:] if n > 100 else b).tobytes()))
+    assert gpu.crc32c_dev(bufs) == want

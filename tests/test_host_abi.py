@@ -99,3 +99,11 @@ def test_no_cpu_fallback_in_product_path():
                 src = open(os.path.join(dirpath, f)).read()
                 assert "import oracle" not in src and "from oracle" not in src, f
                 assert "liboracle" not in src, f
+
+
+def test_host_crc32c_helper(orc, golden):
+    import dlsm_amd
+
+    for c in golden["full"]["crc32c"]:
+        assert dlsm_amd.crc32c(bytes.fromhex(c["data"])) == c["crc"]
+    assert dlsm_amd.crc32c_mask(dlsm_amd.crc32c(b"foo")) == orc.crc32c_mask(orc.crc32c(b"foo"))
