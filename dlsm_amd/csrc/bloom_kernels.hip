@@ -23,6 +23,8 @@
 //   legacy CreateFilter      util/bloom.cc:25-55, KeyMayMatch :57-81
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bloom_internal.h"
 
 namespace dlsm {
@@ -445,8 +447,9 @@ __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint
 // with 16-byte stores.
 // ---------------------------------------------------------------------------
 constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
-constexpr int kProbeSliceBlock = 1024;  // probe slices (64 KiB LDS -> 2 per CU, 32 waves)
-constexpr int kWalkU = 8;               // hashes in flight per lane in the segment walks
+// probe slices: 64 KiB LDS per workgroup, 512 or 1024 threads (launch_probe_slices)
+constexpr int kWalkU = 8;               // hashes in flight per lane (build segment walk)
+constexpr int kProbeWalkU = 6;          // probe walk: 6 keeps 2 x 1024-thread groups per CU (<= 64 VGPRs)
 
 template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
@@ -704,14 +707,14 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
 // the chunks); the slice sits in LDS, waves walk the slice's segments of 64
 // chunks at a time with 4 hashes in flight per lane.  smask gets each key's
 // F-bit answer at the key's bucketed position.
-template <int LGR, int K>
-__global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
+template <int LGR, int K, int NT>
+__global__ __launch_bounds__(NT) void probe_slice_kernel(
     const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
-  constexpr int U = kWalkU;
-  constexpr int NW = kProbeSliceBlock / 64;
+  constexpr int U = kProbeWalkU;
+  constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint64_t sl[R * 64];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t s = blockIdx.x % S;
@@ -720,19 +723,16 @@ __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
   const uint32_t nl = min(R, L - lo_line);
   {
     // all of the slice's 16-byte loads in flight before the first LDS store
-    constexpr int V = R * 32 / kProbeSliceBlock;
+    constexpr int V = R * 32 / NT;
     const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 64u);
     uint4* dst = reinterpret_cast<uint4*>(sl);
     const uint32_t nw = nl * 32u;
-    uint4 t0 = src[min(static_cast<uint32_t>(0 * kProbeSliceBlock + tid), nw - 1u)];
-    uint4 t1 = src[min(static_cast<uint32_t>(1 * kProbeSliceBlock + tid), nw - 1u)];
-    uint4 t2 = src[min(static_cast<uint32_t>(2 * kProbeSliceBlock + tid), nw - 1u)];
-    uint4 t3 = src[min(static_cast<uint32_t>(3 * kProbeSliceBlock + tid), nw - 1u)];
-    static_assert(V == 4, "prologue written for 4 x 16 B per thread");
-    if (0 * kProbeSliceBlock + tid < nw) dst[0 * kProbeSliceBlock + tid] = t0;
-    if (1 * kProbeSliceBlock + tid < nw) dst[1 * kProbeSliceBlock + tid] = t1;
-    if (2 * kProbeSliceBlock + tid < nw) dst[2 * kProbeSliceBlock + tid] = t2;
-    if (3 * kProbeSliceBlock + tid < nw) dst[3 * kProbeSliceBlock + tid] = t3;
+    uint4 t[V];
+#pragma unroll
+    for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
+#pragma unroll
+    for (int v = 0; v < V; v++)
+      if (static_cast<uint32_t>(v * NT + tid) < nw) dst[v * NT + tid] = t[v];
   }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
@@ -747,9 +747,11 @@ __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
     const uint32_t excl = incl - cnt;
     const uint32_t T = __shfl(incl, 63, 64);
     uint32_t sc = 0;
+    const uint32_t* gent = entries + static_cast<uint64_t>(g) * kProbeChunk;  // group base
+    uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
     for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
       uint32_t hv[U];
-      uint64_t idx[U];
+      uint32_t idx[U];  // offset inside the group's 64 chunk regions (< 2^18)
       bool ok[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -758,8 +760,8 @@ __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
         uint32_t li = 0, st = 0, of = 0;
         if (b0 < T) seg_locate(excl, o0, T, b0, sc, li, st, of);
         const uint32_t ec = min(b0 + lane, T - 1u);
-        idx[u] = static_cast<uint64_t>(g + li) * kProbeChunk + of + (ec - st);
-        hv[u] = entries[idx[u]];  // valid for every lane (clamped e): no select around the load
+        idx[u] = li * kProbeChunk + of + (ec - st);
+        hv[u] = gent[idx[u]];  // valid for every lane (clamped e): no select around the load
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(kProbeSliceBlock, 8) void probe_slice_kernel(
           }
         }
         acc &= 0x0101010101010101ull;
-        smask[idx[u]] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
+        gmask[idx[u]] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
       }
     }
   }
@@ -998,12 +1000,22 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
                                const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
   if (lgR != 7) return hipErrorInvalidValue;
-  if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
-    probe_slice_kernel<7, 6><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(
-        stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
-  else
-    probe_slice_kernel<7, 0><<<n_slices * parts, kProbeSliceBlock, 0, s>>>(
-        stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
+  static const int nt = [] {
+    const char* e = getenv("DLSM_PROBE_SLICE_THREADS");
+    return e && atoi(e) == 512 ? 512 : 1024;
+  }();
+#define DLSM_PROBE_SLICE(KK, NTT)                                                        \
+  probe_slice_kernel<7, KK, NTT><<<n_slices * parts, NTT, 0, s>>>(stacked, L, magic, k, \
+                                                                   n_slices, n_chunks, entries, tab, \
+                                                                   smask, parts)
+  if (k == 6) {  // bits_per_key 10 (ChooseNumProbes)
+    if (nt == 512) DLSM_PROBE_SLICE(6, 512);
+    else DLSM_PROBE_SLICE(6, 1024);
+  } else {
+    if (nt == 512) DLSM_PROBE_SLICE(0, 512);
+    else DLSM_PROBE_SLICE(0, 1024);
+  }
+#undef DLSM_PROBE_SLICE
   return hipGetLastError();
 }
 
