@@ -312,31 +312,41 @@ __device__ __forceinline__ uint32_t chunk_distinct(const uint32_t (&h)[PER], uin
 
 // Segment walk over one group of up to 64 chunks.  Lane l holds segment l's
 // flat start `excl` (non-decreasing; empty and out-of-range segments repeat
-// the next start) and its offset `off` inside chunk l's region.  For the batch
-// of flat entries [b0, b0+64) (b0 uniform) each lane finds the segment holding
-// its entry min(b0+lane, T-1).  `sc` (uniform) carries the segment of the batch
-// start from batch to batch.  Only v_readlane + compares: the ~4 segment
-// boundaries inside a batch cost a few VALU ops, no LDS round trips.
-__device__ __forceinline__ void seg_locate(uint32_t excl, uint32_t off, uint32_t T, uint32_t b0,
-                                           uint32_t& sc, uint32_t& li, uint32_t& st,
-                                           uint32_t& of) {
-  while (sc + 1 < 64 && static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, sc + 1)) <= b0) sc++;
+// the next start) and its offset `off` inside chunk l's region.  For U batches
+// of 64 consecutive flat entries (batch u starts at uniform b0 + 64u), every
+// lane finds the segment holding its entry e = min(b0 + 64u + lane, T-1) --
+// the largest l with excl[l] <= e -- by U binary searches over the wave
+// (ds_bpermute), issued step-major so the U searches advance together: 6
+// dependent rounds of U independent permutes, then 2 rounds for (start, off).
+// Returns each lane's in-group entry offset li*C + off + (e - start).
+template <int U, uint32_t CHUNK>
+__device__ __forceinline__ void seg_locate_batch(uint32_t excl, uint32_t off, uint32_t T,
+                                                 uint32_t b0, uint32_t (&idx)[U]) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t e = min(b0 + lane, T - 1u);
-  const uint32_t last = min(b0 + 63u, T - 1u);
-  li = sc;
-  st = static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, sc));
-  of = static_cast<uint32_t>(__builtin_amdgcn_readlane(off, sc));
-  for (uint32_t j = sc + 1; j < 64; j++) {
-    const uint32_t bj = static_cast<uint32_t>(__builtin_amdgcn_readlane(excl, j));
-    if (bj > last) break;
-    const uint32_t oj = static_cast<uint32_t>(__builtin_amdgcn_readlane(off, j));
-    if (e >= bj) {
-      li = j;
-      st = bj;
-      of = oj;
-    }
+  uint32_t e[U];
+  int lo[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    e[u] = min(b0 + u * 64u + lane, T - 1u);
+    lo[u] = 0;
   }
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) {
+    uint32_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = __shfl(excl, lo[u] + step, 64);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (v[u] <= e[u]) lo[u] += step;
+  }
+  uint32_t st[U], of[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    st[u] = __shfl(excl, lo[u], 64);
+    of[u] = __shfl(off, lo[u], 64);
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) idx[u] = static_cast<uint32_t>(lo[u]) * CHUNK + of[u] + (e[u] - st[u]);
 }
 
 // Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
@@ -491,19 +501,15 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t excl = incl - cnt;
         const uint32_t T = __shfl(incl, 63, 64);
-        uint32_t sc = 0;
+        const uint32_t* gent = ent + static_cast<uint64_t>(g) * kBuildChunk;
         for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
-          uint32_t hv[U];
+          uint32_t idx[U], hv[U];
           bool ok[U];
+          seg_locate_batch<U, kBuildChunk>(excl, o0, T, e0, idx);
 #pragma unroll
           for (int u = 0; u < U; u++) {
-            const uint32_t b0 = e0 + u * 64u;
-            ok[u] = b0 + lane < T;
-            uint32_t li = 0, st = 0, of = 0;
-            if (b0 < T) seg_locate(excl, o0, T, b0, sc, li, st, of);
-            const uint32_t ec = min(b0 + lane, T - 1u);
-            const uint64_t idx = static_cast<uint64_t>(g + li) * kBuildChunk + of + (ec - st);
-            hv[u] = ent[idx];  // valid for every lane (clamped e): no select around the load
+            ok[u] = e0 + u * 64u + lane < T;
+            hv[u] = gent[idx[u]];  // valid for every lane (clamped e): no select around the load
           }
 #pragma unroll
           for (int u = 0; u < U; u++)
@@ -746,25 +752,20 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t excl = incl - cnt;
     const uint32_t T = __shfl(incl, 63, 64);
-    uint32_t sc = 0;
     const uint32_t* gent = entries + static_cast<uint64_t>(g) * kProbeChunk;  // group base
     uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
     for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
-      uint32_t hv[U];
-      uint32_t idx[U];  // offset inside the group's 64 chunk regions (< 2^18)
+      uint32_t idx[U], hv[U];  // idx: offset inside the group's 64 chunk regions (< 2^18)
       bool ok[U];
+      seg_locate_batch<U, kProbeChunk>(excl, o0, T, e0, idx);
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const uint32_t b0 = e0 + u * 64u;
-        ok[u] = b0 + lane < T;
-        uint32_t li = 0, st = 0, of = 0;
-        if (b0 < T) seg_locate(excl, o0, T, b0, sc, li, st, of);
-        const uint32_t ec = min(b0 + lane, T - 1u);
-        idx[u] = li * kProbeChunk + of + (ec - st);
+        ok[u] = e0 + u * 64u + lane < T;
         hv[u] = gent[idx[u]];  // valid for every lane (clamped e): no select around the load
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
+        // per-hash branch: keeps each hash's k LDS reads (u64) the only ones live
         if (!ok[u]) continue;
         uint32_t x = hv[u];
         const uint64_t* ln = sl + (fastmod(x, L, magic) - lo_line) * 64u;

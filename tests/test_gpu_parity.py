@@ -198,7 +198,7 @@ def test_full_probe_stacked_vs_oracle(gpu, orc, F):
 
     n_per = 200_000
     filters = [orc.full_build(orc.dbbench_keys(f, 8, n_per), n_per) for f in range(F)]
-    nq = 700_001
+    nq = 1_300_001  # > 256 chunks of 4096: every wave of a 1024-thread slice group works
     vals = orc.mt_values(1000, 8 * n_per * 2, nq)
     q = orc.keys_from_values(vals)
     want = orc.full_probe(filters, q, nq, nthreads=8)
