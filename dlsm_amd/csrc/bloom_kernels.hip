@@ -310,43 +310,52 @@ __device__ __forceinline__ uint32_t chunk_distinct(const uint32_t (&h)[PER], uin
   return tot;
 }
 
-// Segment walk over one group of up to 64 chunks.  Lane l holds segment l's
-// flat start `excl` (non-decreasing; empty and out-of-range segments repeat
-// the next start) and its offset `off` inside chunk l's region.  For U batches
-// of 64 consecutive flat entries (batch u starts at uniform b0 + 64u), every
-// lane finds the segment holding its entry e = min(b0 + 64u + lane, T-1) --
-// the largest l with excl[l] <= e -- by U binary searches over the wave
-// (ds_bpermute), issued step-major so the U searches advance together: 6
-// dependent rounds of U independent permutes, then 2 rounds for (start, off).
-// Returns each lane's in-group entry offset li*C + off + (e - start).
-template <int U, uint32_t CHUNK>
-__device__ __forceinline__ void seg_locate_batch(uint32_t excl, uint32_t off, uint32_t T,
-                                                 uint32_t b0, uint32_t (&idx)[U]) {
+// Inclusive max-scan over the wave in DPP: row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast:15 / row_bcast:31 across rows (no LDS traffic).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+  return v;
+}
+
+constexpr uint32_t kWin = 63;  // entries per walk window (lane 63 is the permute sink)
+
+// Segment walk over one group of up to 64 chunks.  Lane l holds segment l:
+// its flat range [excl, incl) inside the group (wave prefix scan of the
+// counts) and its marker dv = l*CHUNK + off - excl + 1, where off is the
+// segment's offset inside chunk l's region; entry e of segment l then sits at
+// in-group offset e + dv - 1, and dv is non-decreasing over the non-empty
+// segments.  For U windows of 63 entries (window u = [w0 + 63u, +63)), each
+// non-empty segment forward-permutes (ds_permute) its marker to the lane where
+// it starts in the window -- lane 0 for the one segment holding the window's
+// first entry -- and every other segment to lane 63, which is never read.  At
+// most one segment lands on each of lanes 0..62, so the result does not
+// depend on how the permute resolves collisions; an inclusive max-scan then
+// hands each lane the marker of its own segment.  One permute + 6 DPP steps
+// per window instead of a 6-step binary search.  Lanes past T (or lane 63)
+// get the window's first entry, so every index stays inside the group.
+template <int U>
+__device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t incl, uint32_t dv,
+                                               uint32_t T, uint32_t w0, uint32_t (&idx)[U],
+                                               bool (&ok)[U]) {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t e[U];
-  int lo[U];
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    e[u] = min(b0 + u * 64u + lane, T - 1u);
-    lo[u] = 0;
+    const uint32_t w = w0 + u * kWin;
+    uint32_t dst = 63u;
+    if (excl <= w && w < incl) dst = 0u;
+    else if (excl > w && excl < incl && excl - w < kWin) dst = excl - w;
+    const uint32_t m = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_permute(static_cast<int>(dst * 4u), static_cast<int>(dv)));
+    const uint32_t id = w + lane + wave_incl_max(m) - 1u;
+    const uint32_t id0 = w < T ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0)) : 0u;
+    ok[u] = lane < kWin && w + lane < T;
+    idx[u] = ok[u] ? id : id0;
   }
-#pragma unroll
-  for (int step = 32; step > 0; step >>= 1) {
-    uint32_t v[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) v[u] = __shfl(excl, lo[u] + step, 64);
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (v[u] <= e[u]) lo[u] += step;
-  }
-  uint32_t st[U], of[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    st[u] = __shfl(excl, lo[u], 64);
-    of[u] = __shfl(off, lo[u], 64);
-  }
-#pragma unroll
-  for (int u = 0; u < U; u++) idx[u] = static_cast<uint32_t>(lo[u]) * CHUNK + of[u] + (e[u] - st[u]);
 }
 
 // Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
@@ -501,16 +510,14 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
         const uint32_t incl = wave_incl_scan(cnt);
         const uint32_t excl = incl - cnt;
         const uint32_t T = __shfl(incl, 63, 64);
+        const uint32_t dv = lane * kBuildChunk + o0 - excl + 1u;
         const uint32_t* gent = ent + static_cast<uint64_t>(g) * kBuildChunk;
-        for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
+        for (uint32_t e0 = 0; e0 < T; e0 += kWin * U) {
           uint32_t idx[U], hv[U];
           bool ok[U];
-          seg_locate_batch<U, kBuildChunk>(excl, o0, T, e0, idx);
+          seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
 #pragma unroll
-          for (int u = 0; u < U; u++) {
-            ok[u] = e0 + u * 64u + lane < T;
-            hv[u] = gent[idx[u]];  // valid for every lane (clamped e): no select around the load
-          }
+          for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
 #pragma unroll
           for (int u = 0; u < U; u++)
             if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], J.k);
@@ -643,17 +650,25 @@ __global__ __launch_bounds__(kBlock) void probe_direct_kernel(const FilterDev* _
 
 // ---------------------------------------------------------------------------
 // Full filter probe, sliced (F <= 8 filters with a common line count / k).
-// Stacked image: u64 word (line*64 + byte) holds byte `byte` of filter f in
-// its byte f, so one 8-byte LDS read answers a probe for all 8 filters.
+// Bit-transposed stacked image: byte (line*512 + bit) holds bit `bit` of line
+// `line` of filter f in its bit f, so one 1-byte LDS read answers a probe for
+// all 8 filters and ANDing the k bytes gives the key's answer byte directly.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* __restrict__ fs,
                                                                int F, uint64_t words,
                                                                uint64_t* __restrict__ stacked) {
   for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; w < words;
        w += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    uint64_t v = 0;
-    for (int f = 0; f < F; f++) v |= static_cast<uint64_t>(fs[f].data[w]) << (8 * f);
-    stacked[w] = v;
+    uint64_t x = 0;  // byte f = byte w of filter f
+    for (int f = 0; f < F; f++) x |= static_cast<uint64_t>(fs[f].data[w]) << (8 * f);
+    // 8x8 bit transpose: bit b of byte f -> bit f of byte b
+    uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
+    x ^= t ^ (t << 7);
+    t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
+    x ^= t ^ (t << 14);
+    t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
+    x ^= t ^ (t << 28);
+    stacked[w] = x;  // bytes w*8 .. w*8+7 = bit positions 8*(w%64) .. +7 of line w/64
   }
 }
 
@@ -709,19 +724,19 @@ __global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
   store_chunk_u16<kPartBlock>(pos + first, rk, nk);
 }
 
-// Pass 2: one 512-thread workgroup per (slice of 2^LGR stacked lines, part of
-// the chunks); the slice sits in LDS, waves walk the slice's segments of 64
-// chunks at a time with 4 hashes in flight per lane.  smask gets each key's
-// F-bit answer at the key's bucketed position.
+// Pass 2: one NT-thread workgroup per (slice of 2^LGR stacked lines, part of
+// the chunks); the slice (64 KiB) sits in LDS, waves walk the slice's
+// segments of 64 chunks at a time, 6 windows of 63 hashes in flight per wave.
+// smask gets each key's F-bit answer at the key's bucketed position.
 template <int LGR, int K, int NT>
 __global__ __launch_bounds__(NT) void probe_slice_kernel(
-    const uint64_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
+    const uint8_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
   constexpr int U = kProbeWalkU;
   constexpr int NW = NT / 64;
-  __shared__ __attribute__((aligned(16))) uint64_t sl[R * 64];
+  __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t s = blockIdx.x % S;
   const uint32_t p = blockIdx.x / S;
@@ -730,7 +745,7 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   {
     // all of the slice's 16-byte loads in flight before the first LDS store
     constexpr int V = R * 32 / NT;
-    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 64u);
+    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 512u);
     uint4* dst = reinterpret_cast<uint4*>(sl);
     const uint32_t nw = nl * 32u;
     uint4 t[V];
@@ -752,47 +767,40 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
     const uint32_t incl = wave_incl_scan(cnt);
     const uint32_t excl = incl - cnt;
     const uint32_t T = __shfl(incl, 63, 64);
+    const uint32_t dv = lane * kProbeChunk + o0 - excl + 1u;
     const uint32_t* gent = entries + static_cast<uint64_t>(g) * kProbeChunk;  // group base
     uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
-    for (uint32_t e0 = 0; e0 < T; e0 += 64u * U) {
+    for (uint32_t e0 = 0; e0 < T; e0 += kWin * U) {
       uint32_t idx[U], hv[U];  // idx: offset inside the group's 64 chunk regions (< 2^18)
       bool ok[U];
-      seg_locate_batch<U, kProbeChunk>(excl, o0, T, e0, idx);
+      seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
+#pragma unroll
+      for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        ok[u] = e0 + u * 64u + lane < T;
-        hv[u] = gent[idx[u]];  // valid for every lane (clamped e): no select around the load
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        // per-hash branch: keeps each hash's k LDS reads (u64) the only ones live
+        // per-hash branch: keeps each hash's k LDS reads the only ones live
         if (!ok[u]) continue;
         uint32_t x = hv[u];
-        const uint64_t* ln = sl + (fastmod(x, L, magic) - lo_line) * 64u;
+        const uint32_t base = (fastmod(x, L, magic) - lo_line) << 9;  // 512 stacked bytes per line
         const uint32_t delta = bloom_delta(x);
-        uint64_t acc = 0x0101010101010101ull;
+        uint32_t acc = 0xffu;
         if constexpr (K > 0) {
           // k known at compile time: all k LDS reads issue back to back
-          uint64_t v[K];
-          uint32_t sh[K];
+          uint32_t v[K];
 #pragma unroll
           for (int q = 0; q < K; q++) {
-            const uint32_t bp = x & 511u;
-            v[q] = ln[bp >> 3];
-            sh[q] = bp & 7u;
+            v[q] = sl[base | (x & 511u)];
             x += delta;
           }
 #pragma unroll
-          for (int q = 0; q < K; q++) acc &= v[q] >> sh[q];
+          for (int q = 0; q < K; q++) acc &= v[q];
         } else {
           for (int q = 0; q < k; q++) {
-            const uint32_t bp = x & 511u;
-            acc &= ln[bp >> 3] >> (bp & 7u);
+            acc &= sl[base | (x & 511u)];
             x += delta;
           }
         }
-        acc &= 0x0101010101010101ull;
-        gmask[idx[u]] = static_cast<uint8_t>((acc * 0x0102040810204080ull) >> 56);
+        gmask[idx[u]] = static_cast<uint8_t>(acc);
       }
     }
   }
@@ -1006,9 +1014,9 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
     return e && atoi(e) == 512 ? 512 : 1024;
   }();
 #define DLSM_PROBE_SLICE(KK, NTT)                                                        \
-  probe_slice_kernel<7, KK, NTT><<<n_slices * parts, NTT, 0, s>>>(stacked, L, magic, k, \
-                                                                   n_slices, n_chunks, entries, tab, \
-                                                                   smask, parts)
+  probe_slice_kernel<7, KK, NTT><<<n_slices * parts, NTT, 0, s>>>(                        \
+      reinterpret_cast<const uint8_t*>(stacked), L, magic, k, n_slices, n_chunks, entries, \
+      tab, smask, parts)
   if (k == 6) {  // bits_per_key 10 (ChooseNumProbes)
     if (nt == 512) DLSM_PROBE_SLICE(6, 512);
     else DLSM_PROBE_SLICE(6, 1024);
