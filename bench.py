@@ -54,6 +54,9 @@ def main():
     ap.add_argument("--filters", type=int, default=8)
     ap.add_argument("--bits-per-key", type=int, default=10)
     ap.add_argument("--path", type=int, default=0, help="0 auto, 1 direct, 2 sliced")
+    ap.add_argument("--probe-round", type=int, default=None,
+                    help="keys per pipelined probe round (0 = one round, the default)")
+    ap.add_argument("--build-groups", type=int, default=0, help="pipelined build job groups (0/1 = one group)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-probe-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
@@ -81,6 +84,9 @@ def main():
     N, T, Q, F, bpk = args.keys_per_table, args.tables, args.lookups, args.filters, args.bits_per_key
     ctx = dlsm_amd.Context(local)
     ctx.set_path(args.path)
+    if args.probe_round is not None:
+        ctx.set_probe_round(args.probe_round)
+    ctx.set_build_groups(args.build_groups)
     stream = torch.cuda.Stream(device=dev)
     ctx.set_stream(stream)
 
@@ -172,6 +178,7 @@ def main():
             "key_bytes": 20, "bits_per_key": bpk, "tables": T, "keys_per_table": N,
             "lookups": Q, "filters": F, "parallelism": f"sstable-sharded x{world}, no collective",
             "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
+            "probe_round_keys": args.probe_round, "build_groups": args.build_groups,
         },
         "roofline": {
             "bound": "hbm", "kernel": f"{dominant} pass", "achieved": round(ach, 1),

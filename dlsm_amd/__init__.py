@@ -31,6 +31,7 @@ __all__ = [
 ]
 
 PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
+OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 
 
 def lib():
@@ -181,6 +182,17 @@ class Context:
 
     def set_path(self, path: int):
         check(lib().dlsm_ctx_set_path(self.h, path), "set_path")
+
+    def set_option(self, option: int, value: int):
+        check(lib().dlsm_ctx_set_option(self.h, option, value), "set_option")
+
+    def set_probe_round(self, keys: int):
+        """Keys per pipelined probe round (0 = one round)."""
+        self.set_option(OPT_PROBE_ROUND_KEYS, keys)
+
+    def set_build_groups(self, groups: int):
+        """Job groups of a pipelined build (0 = auto, 1..4)."""
+        self.set_option(OPT_BUILD_GROUPS, groups)
 
     def set_stream(self, stream=None):
         """Run on a torch.cuda.Stream (or its raw handle); None = own stream."""

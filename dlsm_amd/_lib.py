@@ -56,6 +56,7 @@ SIGNATURES = [
     ("dlsm_ctx_sync", C.c_int, [_VP]),
     ("dlsm_ctx_reserve", C.c_int, [_VP, C.c_uint64, C.c_uint32]),
     ("dlsm_ctx_set_path", C.c_int, [_VP, C.c_int]),
+    ("dlsm_ctx_set_option", C.c_int, [_VP, C.c_int, C.c_uint64]),
     ("dlsm_host_register", C.c_int, [_VP, C.c_size_t]),
     ("dlsm_host_unregister", C.c_int, [_VP]),
     ("dlsm_bloom_full_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),

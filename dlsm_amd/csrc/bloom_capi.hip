@@ -69,11 +69,27 @@ uint32_t ceil_div_u32(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a 
 
 }  // namespace
 
+// Pipelined passes (opt-in knobs).  Probe: round r+1's partition runs on a
+// helper stream while the context stream runs round r's slice + unpermute,
+// over kProbeBufs rotating intermediate buffers.  Build: job group g+1's
+// partition overlaps group g's slices the same way.  The context stream's last
+// command depends on every helper command, so a call needs no separate join.
+// Off by default: measured on MI355X (profiles/r01_v12_*), the overlapped
+// kernels each ran ~2x slower (the slice passes fill every wave slot of a CU)
+// and every round added ~10 us of launch gaps, a net loss.
+constexpr int kProbeBufs = 3;
+constexpr int kStageEvents = 4;
+
 struct dlsm_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
+  hipStream_t aux = nullptr;              // helper stream of the pipelined passes
+  hipEvent_t ev_fork = nullptr;           // context stream -> helper
+  hipEvent_t ev_part[kStageEvents] = {};  // partition of buffer / group b done (helper)
+  hipEvent_t ev_free[kStageEvents] = {};  // buffer b consumed (context stream)
   int path = 0;
+  int build_groups = 1;     // job groups of a build (1 = one partition + one slice launch)
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   // build workspace
   DevBuf<uint32_t> entries;
@@ -165,6 +181,21 @@ int choose_build_lgR(const std::vector<uint32_t>& Ls) {
     if (ok) return lg;
   }
   return -1;
+}
+
+// The helper stream starts behind everything already queued on the context
+// stream (the call's inputs).
+int fork_aux(dlsm_ctx* ctx) {
+  DLSM_TRY(hipEventRecord(ctx->ev_fork, ctx->stream));
+  DLSM_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+  return DLSM_OK;
+}
+
+// `to` waits for everything queued on `from` so far.
+int hand_over(hipStream_t from, hipStream_t to, hipEvent_t ev) {
+  DLSM_TRY(hipEventRecord(ev, from));
+  DLSM_TRY(hipStreamWaitEvent(to, ev, 0));
+  return DLSM_OK;
 }
 
 // FullFilterBlockReader ctor checks (table/full_filter_block.cc:186-252) on the
@@ -261,13 +292,18 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (!ctx) return DLSM_E_NOMEM;
   ctx->device = device;
   hipError_t e = hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    delete ctx;
-    return from_hip(e);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  for (int b = 0; b < kStageEvents && e == hipSuccess; b++) {
+    e = hipEventCreateWithFlags(&ctx->ev_part[b], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_free[b], hipEventDisableTiming);
   }
   ctx->stream = ctx->own;
-  ctx->probe_round = 0;
-  if (const char* e = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(e, nullptr, 10);
+  if (e != hipSuccess) {
+    dlsm_ctx_destroy(ctx);
+    return from_hip(e);
+  }
+  if (const char* v = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(v, nullptr, 10);
   *out = ctx;
   return DLSM_OK;
 }
@@ -275,7 +311,8 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
 int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   if (!ctx) return DLSM_OK;
   DeviceGuard g(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
   ctx->entries.release();
   ctx->tab.release();
   ctx->jobs.release();
@@ -296,6 +333,12 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->crc_outp.release();
   ctx->crc_cap.release();
   ctx->crc_val.release();
+  if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  for (int b = 0; b < kStageEvents; b++) {
+    if (ctx->ev_part[b]) (void)hipEventDestroy(ctx->ev_part[b]);
+    if (ctx->ev_free[b]) (void)hipEventDestroy(ctx->ev_free[b]);
+  }
+  if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return DLSM_OK;
@@ -320,6 +363,23 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path) {
   if (!ctx || path < 0 || path > 2) return DLSM_E_ARG;
   ctx->path = path;
   return DLSM_OK;
+}
+
+int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
+  if (!ctx) return DLSM_E_ARG;
+  switch (option) {
+    case DLSM_OPT_PATH:
+      return value > 2 ? DLSM_E_ARG : dlsm_ctx_set_path(ctx, static_cast<int>(value));
+    case DLSM_OPT_PROBE_ROUND_KEYS:
+      ctx->probe_round = value;
+      return DLSM_OK;
+    case DLSM_OPT_BUILD_GROUPS:
+      if (value > static_cast<uint64_t>(kStageEvents)) return DLSM_E_ARG;
+      ctx->build_groups = value ? static_cast<int>(value) : 1;
+      return DLSM_OK;
+    default:
+      return DLSM_E_ARG;
+  }
 }
 
 int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
@@ -422,10 +482,27 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   if (sliced_ok) {
     DLSM_CHECK(ctx->entries.ensure(entry));
     DLSM_CHECK(ctx->tab.ensure(tabw));
-    DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p,
-                                   ctx->entries.p, ctx->tab.p, lgR, mode, s));
-    DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, slice, ctx->dchunk.p, ctx->entries.p,
-                                ctx->tab.p, lgR, s));
+    // Job groups of about equal chunk counts: group g's partition (HBM-bound)
+    // runs on the helper stream while the context stream runs group g-1's
+    // slices (LDS-bound).
+    const int G = std::max(1, std::min(ctx->build_groups, n_jobs));
+    std::vector<int> cut(1, 0);
+    for (int j = 1; j < n_jobs && static_cast<int>(cut.size()) < G; j++)
+      if (static_cast<uint64_t>(starts[j]) * G >= static_cast<uint64_t>(chunk) * cut.size()) cut.push_back(j);
+    cut.push_back(n_jobs);
+    const int ng = static_cast<int>(cut.size()) - 1;
+    auto chunk_at = [&](int j) { return j < n_jobs ? starts[j] : chunk; };
+    auto slice_at = [&](int j) { return j < n_jobs ? starts[n_jobs + j] : slice; };
+    if (ng > 1) DLSM_CHECK(fork_aux(ctx));
+    for (int g = 0; g < ng; g++) {
+      const uint32_t c0 = chunk_at(cut[g]), s0 = slice_at(cut[g]);
+      DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, c0, chunk_at(cut[g + 1]) - c0,
+                                     ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, mode,
+                                     ng > 1 ? ctx->aux : s));
+      if (ng > 1) DLSM_CHECK(hand_over(ctx->aux, s, ctx->ev_part[g % kStageEvents]));
+      DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, s0, slice_at(cut[g + 1]) - s0,
+                                  ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, s));
+    }
   } else {
     DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, s));
     DLSM_TRY(launch_full_zero(ctx->jobs.p, n_jobs, ctx->dchunk.p, ctx->jobL.p, s));
@@ -764,23 +841,37 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
     return DLSM_OK;
   }
-  // Rounds: the bucketed intermediates (4 B hash + 2 B position + 1 B answer
-  // per key) of one round stay resident in the 256 MiB Infinity Cache, and the
-  // next round overwrites the same lines, so they never stream to HBM.
+  // Rounds of probe_round keys, pipelined: round r's partition (helper
+  // stream) overlaps round r-1's slice + unpermute (context stream).  A
+  // round's intermediates (4 B hash + 2 B position + 1 B answer per key) live
+  // in one of kProbeBufs rotating buffers, small enough to stay resident in
+  // the 256 MiB Infinity Cache while the keys stream past.
   const uint64_t n = keys->n;
   uint64_t round = n;
   if (ctx->probe_round && ctx->probe_round < n)
     round = std::max<uint64_t>(kProbeChunk, (ctx->probe_round / kProbeChunk) * kProbeChunk);
-  const uint64_t rk = std::min(round, n);
-  const uint32_t nCmax = ceil_div_u32(rk, kProbeChunk);
-  DLSM_CHECK(ctx->entries.ensure(rk));
-  DLSM_CHECK(ctx->pos.ensure(rk));
-  DLSM_CHECK(ctx->smask.ensure(rk));
-  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(S + 1) * nCmax));
+  const uint64_t n_rounds = (n + round - 1) / round;
+  const bool pipe = n_rounds > 1;
+  const int nbuf = pipe ? kProbeBufs : 1;
+  const uint32_t nCmax = ceil_div_u32(std::min(round, n), kProbeChunk);
+  const uint64_t kstride = static_cast<uint64_t>(nCmax) * kProbeChunk;  // keys per buffer (16-B aligned)
+  const uint64_t tstride = static_cast<uint64_t>(S + 1) * nCmax;        // table u16 per buffer
+  DLSM_CHECK(ctx->entries.ensure(kstride * nbuf));
+  DLSM_CHECK(ctx->pos.ensure(kstride * nbuf));
+  DLSM_CHECK(ctx->smask.ensure(kstride * nbuf));
+  DLSM_CHECK(ctx->tab.ensure(tstride * nbuf));
   const int lgR = 7;  // kProbeSliceLines
-  for (uint64_t r0 = 0; r0 < n; r0 += round) {
+  if (pipe) DLSM_CHECK(fork_aux(ctx));
+  hipStream_t ps = pipe ? ctx->aux : s;
+  for (uint64_t r = 0; r < n_rounds; r++) {
+    const uint64_t r0 = r * round;
     const uint64_t nr = std::min(round, n - r0);
     const uint32_t nC = ceil_div_u32(nr, kProbeChunk);
+    const int b = static_cast<int>(r % nbuf);
+    uint32_t* ent = ctx->entries.p + b * kstride;
+    uint16_t* pos = ctx->pos.p + b * kstride;
+    uint8_t* sm = ctx->smask.p + b * kstride;
+    uint16_t* tab = ctx->tab.p + b * tstride;
     KeyDesc kr = kd;
     kr.n = nr;
     if (kd.offsets) kr.offsets = kd.offsets + r0;
@@ -789,11 +880,12 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     // KiB slices per CU x 256 CUs), each part at least one 64-chunk group per wave.
     int parts = static_cast<int>(std::max<uint32_t>(1, (512u + S / 2) / S));
     parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 1024)));
-    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ctx->entries.p, ctx->pos.p,
-                                    ctx->tab.p, mode, s));
-    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ctx->entries.p,
-                                 ctx->tab.p, ctx->smask.p, parts, s));
-    DLSM_TRY(launch_probe_unpermute(nr, ctx->pos.p, ctx->smask.p, mask_dev + r0, s));
+    if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
+    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ent, pos, tab, mode, ps));
+    if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
+    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ent, tab, sm, parts, s));
+    DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, s));
+    if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }
   return DLSM_OK;
 }

@@ -69,11 +69,13 @@ hipError_t launch_full_zero(const FullJobDev* jobs, int n_jobs, const uint32_t* 
                             uint32_t* jobL, hipStream_t s);
 hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                uint32_t total_chunks, const uint32_t* jobL, int mode, hipStream_t s);
+// Partition chunks [chunk_first, +n_chunks) / slices [slice_first, +n_slices)
+// of the job table (a contiguous job group of a pipelined build).
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                                 uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
-                                 uint16_t* tab, int lgR, int mode, hipStream_t s);
+                                 uint32_t chunk_first, uint32_t n_chunks, uint32_t* dchunk,
+                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, hipStream_t s);
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
-                              uint32_t total_slices, const uint32_t* dchunk,
+                              uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
                               const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s);
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,

@@ -358,6 +358,96 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t incl, uin
   }
 }
 
+// One wave's walk over a slice's segments in the chunk groups g = g_first,
+// g_first + g_step, ... < g_end (64 chunks per group; chunk-major table rows of
+// `rowlen` u16 bucket offsets, `tb` already offset to the slice's column).
+// Software-pipelined: window set i+1's hash loads (and the next group's table
+// rows, one group ahead) are issued before window set i is consumed, so every
+// wave keeps a set of loads in flight while it works on the previous one --
+// the un-pipelined walk spent most of its cycles waiting on these loads.
+// act(hv[U], idx[U], ok[U], g) consumes one window set of group g.
+template <int U, uint32_t CHUNK>
+struct SegWalk {
+  const uint16_t* tb;
+  const uint32_t* entries;
+  uint32_t rowlen, g_step, g_end;
+  uint32_t g;         // current group (first chunk)
+  uint32_t e0;        // next window start in the current group
+  uint32_t excl, incl, dv, T;
+  uint32_t n0, n1;    // prefetched table row of group g + g_step (this lane's chunk)
+
+  __device__ __forceinline__ void load_rows(uint32_t gg, uint32_t& a0, uint32_t& a1) const {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c = min(gg + lane, g_end - 1u);  // clamped: unconditional loads
+    const uint16_t* r = tb + static_cast<uint64_t>(c) * rowlen;
+    a0 = r[0];
+    a1 = r[1];
+  }
+  __device__ __forceinline__ void setup(uint32_t a0, uint32_t a1) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t cnt = g + lane < g_end ? a1 - a0 : 0u;
+    incl = wave_incl_scan(cnt);
+    excl = incl - cnt;
+    T = __shfl(incl, 63, 64);
+    dv = lane * CHUNK + a0 - excl + 1u;
+    e0 = 0;
+  }
+  __device__ __forceinline__ bool start(uint32_t g_first) {
+    g = g_first;
+    if (g >= g_end) return false;
+    uint32_t a0, a1;
+    load_rows(g, a0, a1);
+    if (g + g_step < g_end) load_rows(g + g_step, n0, n1);
+    setup(a0, a1);
+    return true;
+  }
+  // Locate the next window set; false when the walk is done.
+  __device__ __forceinline__ bool next(uint32_t (&idx)[U], bool (&ok)[U], uint32_t& gset) {
+    while (e0 >= T) {
+      g += g_step;
+      if (g >= g_end) return false;
+      const uint32_t a0 = n0, a1 = n1;
+      if (g + g_step < g_end) load_rows(g + g_step, n0, n1);
+      setup(a0, a1);
+    }
+    seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
+    e0 += kWin * U;
+    gset = g;
+    return true;
+  }
+  __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, uint32_t (&hv)[U]) const {
+    const uint32_t* gent = entries + static_cast<uint64_t>(gset) * CHUNK;
+#pragma unroll
+    for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
+  }
+};
+
+template <int U, uint32_t CHUNK, typename Act>
+__device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
+                                              uint32_t g_first, uint32_t g_step, uint32_t g_end, Act act) {
+  SegWalk<U, CHUNK> w{tb, entries, rowlen, g_step, g_end};
+  if (!w.start(g_first)) return;
+  uint32_t idxA[U], hvA[U], gA;
+  bool okA[U];
+  if (!w.next(idxA, okA, gA)) return;
+  w.fetch(idxA, gA, hvA);
+  while (true) {
+    uint32_t idxB[U], hvB[U], gB;
+    bool okB[U];
+    const bool more = w.next(idxB, okB, gB);
+    if (more) w.fetch(idxB, gB, hvB);
+    act(hvA, idxA, okA, gA);
+    if (!more) break;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      idxA[u] = idxB[u];
+      hvA[u] = hvB[u];
+      okA[u] = okB[u];
+    }
+    gA = gB;
+  }
+}
+
 // Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
 // global base is 16-byte aligned: chunk starts are multiples of 4096 elements).
 template <int NT>
@@ -386,7 +476,7 @@ template <int MODE, bool PART>
 __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
     uint32_t* __restrict__ dchunk, uint32_t* __restrict__ entries, uint16_t* __restrict__ tab,
-    int lgR) {
+    int lgR, uint32_t block0) {
   constexpr int C = kBuildChunk;
   constexpr int PER = C / kPartBlock;
   // key tile (K20), then the staging area of the bucketed hashes (both modes)
@@ -397,10 +487,11 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   __shared__ uint32_t wsum[kPartBlock / 64];
   __shared__ int sj;
   const int tid = threadIdx.x;
-  if (tid == 0) sj = find_job(chunk0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
+  const uint32_t bid = blockIdx.x + block0;  // chunk index over all jobs
+  if (tid == 0) sj = find_job(chunk0s, n_jobs, bid);
   __syncthreads();
   const FullJobDev J = jobs[sj];
-  const uint32_t c = blockIdx.x - J.chunk0;
+  const uint32_t c = bid - J.chunk0;
   const uint64_t first = static_cast<uint64_t>(c) * C;
   const uint64_t left = J.keys.n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
@@ -410,7 +501,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   uint32_t prev0 = ~h[0];
   if (first > 0) prev0 = key_hash<MODE == KM_K20 ? KM_K20 : KM_GENERIC>(J.keys, first - 1);
   const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, __shfl(prev0, 0, 64), lastw, wsum);
-  if (tid == 0) dchunk[blockIdx.x] = cnt;
+  if (tid == 0) dchunk[bid] = cnt;
   if constexpr (!PART) return;
 
   const uint32_t S = J.n_slices;
@@ -474,19 +565,20 @@ template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ slice0s, int n_jobs,
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
-    const uint16_t* __restrict__ tab) {
+    const uint16_t* __restrict__ tab, uint32_t block0) {
   constexpr uint32_t R = 1u << LGR;
   constexpr int U = kWalkU;
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
   __shared__ int sj;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) sj = find_job(slice0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
+  const int tid = threadIdx.x, wv = tid >> 6;
+  const uint32_t bid = blockIdx.x + block0;  // slice index over all jobs
+  if (tid == 0) sj = find_job(slice0s, n_jobs, bid);
   for (uint32_t w = tid; w < R * 16; w += kSliceBlock) sl[w] = 0;
   __syncthreads();
   const FullJobDev J = jobs[sj];
-  const uint32_t s = blockIdx.x - J.slice0;
+  const uint32_t s = bid - J.slice0;
   const uint64_t distinct = job_distinct<kSliceBlock>(J, dchunk, wsum);
   uint32_t total_bits;
   const uint32_t L = full_num_lines(distinct, J.bpk, &total_bits);
@@ -502,27 +594,14 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       const uint32_t nC = J.n_chunks;
       const uint16_t* tb = tab + J.tab0 + s;  // chunk-major rows of n_slices+1 u16
       const uint32_t* ent = entries + J.entry0;
-      for (uint32_t g = wv * 64u; g < nC; g += NW * 64u) {
-        const uint32_t c = g + lane;
-        const uint16_t* r = tb + static_cast<uint64_t>(c) * (J.n_slices + 1);
-        const uint32_t o0 = c < nC ? r[0] : 0u;
-        const uint32_t cnt = c < nC ? r[1] - o0 : 0u;
-        const uint32_t incl = wave_incl_scan(cnt);
-        const uint32_t excl = incl - cnt;
-        const uint32_t T = __shfl(incl, 63, 64);
-        const uint32_t dv = lane * kBuildChunk + o0 - excl + 1u;
-        const uint32_t* gent = ent + static_cast<uint64_t>(g) * kBuildChunk;
-        for (uint32_t e0 = 0; e0 < T; e0 += kWin * U) {
-          uint32_t idx[U], hv[U];
-          bool ok[U];
-          seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
+      const int k = J.k;
+      walk_segments<U, kBuildChunk>(
+          tb, J.n_slices + 1, ent, wv * 64u, NW * 64u, nC,
+          [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
 #pragma unroll
-          for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
-#pragma unroll
-          for (int u = 0; u < U; u++)
-            if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], J.k);
-        }
-      }
+            for (int u = 0; u < U; u++)
+              if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], k);
+          });
     } else {
       // Duplicates lowered the line count below the speculative one: the
       // partition used the wrong modulus, so scan every hash of the job.
@@ -737,7 +816,7 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   constexpr int U = kProbeWalkU;
   constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, wv = tid >> 6;
   const uint32_t s = blockIdx.x % S;
   const uint32_t p = blockIdx.x / S;
   const uint32_t lo_line = s << LGR;
@@ -759,51 +838,37 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
   __syncthreads();
-  for (uint32_t g = c_lo + wv * 64u; g < c_hi; g += NW * 64u) {
-    const uint32_t c = g + lane;
-    const uint16_t* r = tb + static_cast<uint64_t>(c) * (S + 1);
-    const uint32_t o0 = c < c_hi ? r[0] : 0u;
-    const uint32_t cnt = c < c_hi ? r[1] - o0 : 0u;
-    const uint32_t incl = wave_incl_scan(cnt);
-    const uint32_t excl = incl - cnt;
-    const uint32_t T = __shfl(incl, 63, 64);
-    const uint32_t dv = lane * kProbeChunk + o0 - excl + 1u;
-    const uint32_t* gent = entries + static_cast<uint64_t>(g) * kProbeChunk;  // group base
-    uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
-    for (uint32_t e0 = 0; e0 < T; e0 += kWin * U) {
-      uint32_t idx[U], hv[U];  // idx: offset inside the group's 64 chunk regions (< 2^18)
-      bool ok[U];
-      seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
+  walk_segments<U, kProbeChunk>(
+      tb, S + 1, entries, c_lo + wv * 64u, NW * 64u, c_hi,
+      [&](const uint32_t (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
+        uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
 #pragma unroll
-      for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
+        for (int u = 0; u < U; u++) {
+          // per-hash branch: keeps each hash's k LDS reads the only ones live
+          if (!ok[u]) continue;
+          uint32_t x = hv[u];
+          const uint32_t base = (fastmod(x, L, magic) - lo_line) << 9;  // 512 stacked bytes per line
+          const uint32_t delta = bloom_delta(x);
+          uint32_t acc = 0xffu;
+          if constexpr (K > 0) {
+            // k known at compile time: all k LDS reads issue back to back
+            uint32_t v[K];
 #pragma unroll
-      for (int u = 0; u < U; u++) {
-        // per-hash branch: keeps each hash's k LDS reads the only ones live
-        if (!ok[u]) continue;
-        uint32_t x = hv[u];
-        const uint32_t base = (fastmod(x, L, magic) - lo_line) << 9;  // 512 stacked bytes per line
-        const uint32_t delta = bloom_delta(x);
-        uint32_t acc = 0xffu;
-        if constexpr (K > 0) {
-          // k known at compile time: all k LDS reads issue back to back
-          uint32_t v[K];
+            for (int q = 0; q < K; q++) {
+              v[q] = sl[base | (x & 511u)];
+              x += delta;
+            }
 #pragma unroll
-          for (int q = 0; q < K; q++) {
-            v[q] = sl[base | (x & 511u)];
-            x += delta;
+            for (int q = 0; q < K; q++) acc &= v[q];
+          } else {
+            for (int q = 0; q < k; q++) {
+              acc &= sl[base | (x & 511u)];
+              x += delta;
+            }
           }
-#pragma unroll
-          for (int q = 0; q < K; q++) acc &= v[q];
-        } else {
-          for (int q = 0; q < k; q++) {
-            acc &= sl[base | (x & 511u)];
-            x += delta;
-          }
+          gmask[idx[u]] = static_cast<uint8_t>(acc);
         }
-        gmask[idx[u]] = static_cast<uint8_t>(acc);
-      }
-    }
-  }
+      });
 }
 
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
@@ -915,10 +980,10 @@ hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, in
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
     full_partition_kernel<KM_K20, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
-                                                                          nullptr, nullptr, 0);
+                                                                          nullptr, nullptr, 0, 0u);
   else
     full_partition_kernel<KM_GENERIC, false><<<total_chunks, kPartBlock, 0, s>>>(
-        jobs, chunk0s, n_jobs, dchunk, nullptr, nullptr, 0);
+        jobs, chunk0s, n_jobs, dchunk, nullptr, nullptr, 0, 0u);
   return hipGetLastError();
 }
 
@@ -940,31 +1005,34 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
 }
 
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
-                                 uint32_t total_chunks, uint32_t* dchunk, uint32_t* entries,
-                                 uint16_t* tab, int lgR, int mode, hipStream_t s) {
-  if (total_chunks == 0) return hipSuccess;
+                                 uint32_t chunk_first, uint32_t n_chunks, uint32_t* dchunk,
+                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
-    full_partition_kernel<KM_K20, true><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
-                                                                         entries, tab, lgR);
+    full_partition_kernel<KM_K20, true><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
+                                                                     entries, tab, lgR, chunk_first);
   else
-    full_partition_kernel<KM_GENERIC, true><<<total_chunks, kPartBlock, 0, s>>>(
-        jobs, chunk0s, n_jobs, dchunk, entries, tab, lgR);
+    full_partition_kernel<KM_GENERIC, true><<<n_chunks, kPartBlock, 0, s>>>(
+        jobs, chunk0s, n_jobs, dchunk, entries, tab, lgR, chunk_first);
   return hipGetLastError();
 }
 
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
-                              uint32_t total_slices, const uint32_t* dchunk,
+                              uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
                               const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s) {
-  if (total_slices == 0) return hipSuccess;
+  if (n_slices == 0) return hipSuccess;
   switch (lgR) {
     case 9:
-      full_slice_kernel<9><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
+      full_slice_kernel<9><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
+                                                            slice_first);
       break;
     case 10:
-      full_slice_kernel<10><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
+      full_slice_kernel<10><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
+                                                             slice_first);
       break;
     case 11:
-      full_slice_kernel<11><<<total_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab);
+      full_slice_kernel<11><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
+                                                             slice_first);
       break;
     default:
       return hipErrorInvalidValue;

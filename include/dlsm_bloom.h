@@ -116,6 +116,16 @@ int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs);
  * 2 = sliced (LDS-tiled).  For A/B measurement; results are identical. */
 int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 
+/* Scheduling knobs; results never depend on them.
+ *   DLSM_OPT_PATH             same as dlsm_ctx_set_path
+ *   DLSM_OPT_PROBE_ROUND_KEYS keys per pipelined probe round (default 0 = one
+ *                             round, or $DLSM_PROBE_ROUND_KEYS)
+ *   DLSM_OPT_BUILD_GROUPS     job groups of a pipelined build (0/1 = one, up to 4) */
+#define DLSM_OPT_PATH 0
+#define DLSM_OPT_PROBE_ROUND_KEYS 1
+#define DLSM_OPT_BUILD_GROUPS 2
+int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
+
 /* Page-lock a host range (e.g. an RDMA-registered FilterChunk slot) so D2H
  * copies land in it directly. */
 int dlsm_host_register(void* p, size_t len);

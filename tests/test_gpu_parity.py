@@ -212,6 +212,73 @@ def test_full_probe_stacked_vs_oracle(gpu, orc, F):
     assert ((want & 1)[vals % 8 == 0][vals[vals % 8 == 0] < 8 * n_per] == 1).all()
 
 
+@pytest.mark.parametrize("round_keys", [0, 4096, 4096 * 37, 4096 * 100])
+def test_full_probe_pipelined_rounds(gpu, orc, round_keys):
+    """Probe rounds pipelined over two streams and three rotating buffers
+    (round r's partition beside round r-1's slices): any round size gives the
+    oracle's masks, including a ragged last round."""
+    import torch
+
+    import dlsm_amd
+
+    n_per = 100_000
+    filters = [orc.full_build(orc.dbbench_keys(f, 8, n_per), n_per) for f in range(8)]
+    nq = 1_000_003 if round_keys != 4096 else 40_961
+    q = orc.keys_from_values(orc.mt_values(77, 8 * n_per * 2, nq))
+    want = orc.full_probe(filters, q, nq, nthreads=8)
+    fs = gpu.filterset(filters)
+    qd = torch.from_numpy(q).cuda()
+    mask = torch.full((nq,), 0xEE, dtype=torch.uint8, device="cuda")
+    gpu.set_probe_round(round_keys)
+    try:
+        gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
+        gpu.sync()
+    finally:
+        gpu.set_probe_round(4 << 20)
+    assert np.array_equal(mask.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("groups", [1, 2, 3, 4])
+def test_full_build_pipelined_groups(gpu, orc, groups):
+    """Job groups pipelined over two streams (group g's partition beside group
+    g-1's slices), uneven table sizes, dev and host entry points."""
+    import torch
+
+    import dlsm_amd
+
+    sizes = [153_846, 1, 0, 600_000, 77_777, 153_846, 4096, 300_001, 12]
+    tables, outs, want = [], [], []
+    for s, n in enumerate(sizes):
+        k = orc.dbbench_keys(s, len(sizes), n) if n else np.zeros(20, np.uint8)
+        want.append(orc.full_build(k, n))
+        tables.append(dlsm_amd.Keys(torch.from_numpy(k).cuda(), n, 20))
+        outs.append(torch.full((dlsm_amd.full_size(n)[0] + 32,), 0xEE, dtype=torch.uint8, device="cuda"))
+    lens = torch.zeros(len(sizes), dtype=torch.uint64, device="cuda")
+    gpu.set_build_groups(groups)
+    try:
+        gpu.full_build_dev(tables, outs, lens, 10)
+        gpu.sync()
+        host = gpu.full_build([dlsm_amd.Keys(t.data.cpu().numpy(), t.n, 20) for t in tables], 10)
+    finally:
+        gpu.set_build_groups(0)
+    L = lens.cpu().numpy()
+    for j, w in enumerate(want):
+        assert int(L[j]) == len(w), j
+        assert outs[j][: int(L[j])].cpu().numpy().tobytes() == w, (j, groups)
+        assert host[j] == w, (j, groups)
+
+
+def test_set_option_rejects_bad_values(gpu):
+    import dlsm_amd
+
+    with pytest.raises(dlsm_amd.DlsmError):
+        gpu.set_build_groups(5)
+    with pytest.raises(dlsm_amd.DlsmError):
+        gpu.set_option(99, 1)
+    with pytest.raises(dlsm_amd.DlsmError):
+        gpu.set_option(dlsm_amd.OPT_PATH, 3)
+
+
 def test_full_probe_many_filters_and_varlen(gpu, orc):
     import dlsm_amd
 
