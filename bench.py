@@ -57,6 +57,14 @@ def main():
     ap.add_argument("--probe-round", type=int, default=None,
                     help="keys per pipelined probe round (0 = one round, the default)")
     ap.add_argument("--build-groups", type=int, default=0, help="pipelined build job groups (0/1 = one group)")
+    ap.add_argument("--probe-chunk-lg", type=int, default=13,
+                    help="log2 keys per probe partition chunk (12..14; library default 13)")
+    ap.add_argument("--probe-slice-lg", type=int, default=7,
+                    help="log2 stacked lines per probe LDS slice (7, 8; library default 7)")
+    ap.add_argument("--traffic", default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                      "profiles", "traffic.json"),
+                    help="PMC traffic summary (scripts/pmc_traffic.py) reported as roofline.traffic "
+                         "when its config matches this run")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-probe-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
@@ -87,6 +95,7 @@ def main():
     if args.probe_round is not None:
         ctx.set_probe_round(args.probe_round)
     ctx.set_build_groups(args.build_groups)
+    ctx.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
     stream = torch.cuda.Stream(device=dev)
     ctx.set_stream(stream)
 
@@ -179,6 +188,7 @@ def main():
             "lookups": Q, "filters": F, "parallelism": f"sstable-sharded x{world}, no collective",
             "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
             "probe_round_keys": args.probe_round, "build_groups": args.build_groups,
+            "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {
             "bound": "hbm", "kernel": f"{dominant} pass", "achieved": round(ach, 1),
@@ -190,6 +200,14 @@ def main():
         "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(Q / probe_ms / 1e3, 1),
                   "alg_GBs": round(probe_gbs, 1), "alg_bytes_per_key": round(probe_bytes / Q, 3)},
     }
+
+    traffic = load_traffic(args.traffic, result["config"], dominant)
+    if traffic:
+        result["roofline"]["traffic"] = traffic["traffic_bytes"]
+        result["roofline"]["traffic_source"] = traffic["source"]
+        result["roofline"]["traffic_alg_ratio"] = round(
+            traffic["traffic_bytes"] / (probe_bytes if dominant == "probe" else build_bytes), 3)
+    result["roofline"]["hbm_copy_GBs_measured"] = round(copy_bandwidth(dev, stream), 1)
 
     # ---- host-inclusive (PCIe) rate, N=1 only: recorded, never `value` ----
     if world == 1 and not args.no_e2e:
@@ -204,6 +222,39 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def load_traffic(path, config, dominant):
+    """Per-launch fabric bytes of the dominant pass from a committed PMC
+    summary (scripts/pmc_traffic.py), only if it was collected on this config."""
+    try:
+        t = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if any(t["config"].get(k) != config.get(k) for k in t["config"]):
+        return None
+    d = t.get(dominant)
+    return {"traffic_bytes": d["traffic_bytes"], "source": t["source"]} if d else None
+
+
+def copy_bandwidth(dev, stream, nbytes=1 << 30, reps=10):
+    """Measured device-to-device streaming rate (read + write bytes / s, GB/s)
+    on this box: the achievable HBM ceiling beside the 8 TB/s spec peak."""
+    import torch
+
+    with torch.cuda.stream(stream):
+        a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            b.copy_(a)
+        e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):

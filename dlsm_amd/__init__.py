@@ -32,6 +32,7 @@ __all__ = [
 
 PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
+OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG = 3, 4
 
 
 def lib():
@@ -193,6 +194,12 @@ class Context:
     def set_build_groups(self, groups: int):
         """Job groups of a pipelined build (0 = auto, 1..4)."""
         self.set_option(OPT_BUILD_GROUPS, groups)
+
+    def set_probe_shape(self, chunk_lg: int, slice_lg: int):
+        """Sliced probe shape: 2^chunk_lg keys per partition chunk (12..14),
+        2^slice_lg stacked lines per LDS slice (7 = 64 KiB, 8 = 128 KiB)."""
+        self.set_option(OPT_PROBE_CHUNK_LG, chunk_lg)
+        self.set_option(OPT_PROBE_SLICE_LG, slice_lg)
 
     def set_stream(self, stream=None):
         """Run on a torch.cuda.Stream (or its raw handle); None = own stream."""

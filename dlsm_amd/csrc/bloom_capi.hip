@@ -91,6 +91,8 @@ struct dlsm_ctx {
   int path = 0;
   int build_groups = 1;     // job groups of a build (1 = one partition + one slice launch)
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
+  int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14)
+  int probe_lgr = 7;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -304,6 +306,8 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
     return from_hip(e);
   }
   if (const char* v = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(v, nullptr, 10);
+  if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
+  if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
   *out = ctx;
   return DLSM_OK;
 }
@@ -377,6 +381,14 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > static_cast<uint64_t>(kStageEvents)) return DLSM_E_ARG;
       ctx->build_groups = value ? static_cast<int>(value) : 1;
       return DLSM_OK;
+    case DLSM_OPT_PROBE_CHUNK_LG:
+      if (value < 12 || value > 14) return DLSM_E_ARG;
+      ctx->probe_lgc = static_cast<int>(value);
+      return DLSM_OK;
+    case DLSM_OPT_PROBE_SLICE_LG:
+      if (value < 7 || value > 8) return DLSM_E_ARG;
+      ctx->probe_lgr = static_cast<int>(value);
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -385,9 +397,11 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
 int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   if (!ctx) return DLSM_E_ARG;
   DeviceGuard g(ctx->device);
-  DLSM_CHECK(ctx->entries.ensure(max_keys));
-  DLSM_CHECK(ctx->pos.ensure(max_keys));
-  DLSM_CHECK(ctx->smask.ensure(max_keys));
+  // probe intermediates are sized in whole chunks of up to 2^14 keys
+  const uint64_t pkeys = (max_keys + 16383u) & ~uint64_t(16383u);
+  DLSM_CHECK(ctx->entries.ensure(pkeys));
+  DLSM_CHECK(ctx->pos.ensure(pkeys));
+  DLSM_CHECK(ctx->smask.ensure(pkeys));
   const uint64_t chunks = (max_keys + kBuildChunk - 1) / kBuildChunk + max_jobs;
   DLSM_CHECK(ctx->tab.ensure(chunks * (kMaxSlices + 1)));
   DLSM_CHECK(ctx->jobs.ensure(max_jobs));
@@ -833,9 +847,18 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   hipStream_t s = ctx->stream;
   const int mode = is_k20(*keys) ? KM_K20 : KM_GENERIC;
   const KeyDesc kd = to_desc(*keys);
-  const uint32_t S = fs->stacked ? ceil_div_u32(fs->L, kProbeSliceLines) : 0;
+  // Slices of 2^lgR stacked lines; a table with more than kMaxSlices slices
+  // of 64 KiB moves to 128 KiB slices (one workgroup per CU).
+  int lgR = ctx->probe_lgr;
+  uint32_t S = fs->stacked ? ceil_div_u32(fs->L, 1u << lgR) : 0;
+  if (S > kMaxSlices && lgR < 8) {
+    lgR = 8;
+    S = ceil_div_u32(fs->L, 1u << lgR);
+  }
+  const int lgC = ctx->probe_lgc;
+  const uint64_t C = 1ull << lgC;
   const bool sliced = ctx->path != 1 && fs->stacked && S >= 1 && S <= kMaxSlices &&
-                      keys->n <= 0xffffffffull * kProbeChunk;
+                      keys->n <= 0xffffffffull * C;
   if (ctx->path == 2 && !sliced) return DLSM_E_ARG;
   if (!sliced) {
     DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
@@ -849,24 +872,23 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   const uint64_t n = keys->n;
   uint64_t round = n;
   if (ctx->probe_round && ctx->probe_round < n)
-    round = std::max<uint64_t>(kProbeChunk, (ctx->probe_round / kProbeChunk) * kProbeChunk);
+    round = std::max<uint64_t>(C, (ctx->probe_round / C) * C);
   const uint64_t n_rounds = (n + round - 1) / round;
   const bool pipe = n_rounds > 1;
   const int nbuf = pipe ? kProbeBufs : 1;
-  const uint32_t nCmax = ceil_div_u32(std::min(round, n), kProbeChunk);
-  const uint64_t kstride = static_cast<uint64_t>(nCmax) * kProbeChunk;  // keys per buffer (16-B aligned)
+  const uint32_t nCmax = ceil_div_u32(std::min(round, n), C);
+  const uint64_t kstride = static_cast<uint64_t>(nCmax) * C;  // keys per buffer (16-B aligned)
   const uint64_t tstride = static_cast<uint64_t>(S + 1) * nCmax;        // table u16 per buffer
   DLSM_CHECK(ctx->entries.ensure(kstride * nbuf));
   DLSM_CHECK(ctx->pos.ensure(kstride * nbuf));
   DLSM_CHECK(ctx->smask.ensure(kstride * nbuf));
   DLSM_CHECK(ctx->tab.ensure(tstride * nbuf));
-  const int lgR = 7;  // kProbeSliceLines
   if (pipe) DLSM_CHECK(fork_aux(ctx));
   hipStream_t ps = pipe ? ctx->aux : s;
   for (uint64_t r = 0; r < n_rounds; r++) {
     const uint64_t r0 = r * round;
     const uint64_t nr = std::min(round, n - r0);
-    const uint32_t nC = ceil_div_u32(nr, kProbeChunk);
+    const uint32_t nC = ceil_div_u32(nr, C);
     const int b = static_cast<int>(r % nbuf);
     uint32_t* ent = ctx->entries.p + b * kstride;
     uint16_t* pos = ctx->pos.p + b * kstride;
@@ -876,15 +898,17 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     kr.n = nr;
     if (kd.offsets) kr.offsets = kd.offsets + r0;
     else kr.bytes = kd.bytes + r0 * kd.key_len;
-    // (slice, part) workgroups: about one resident wave of workgroups (2 x 64
-    // KiB slices per CU x 256 CUs), each part at least one 64-chunk group per wave.
-    int parts = static_cast<int>(std::max<uint32_t>(1, (512u + S / 2) / S));
+    // (slice, part) workgroups: about one resident wave of workgroups (256
+    // CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at least one
+    // 64-chunk group per wave.
+    const uint32_t resident = lgR == 7 ? 512u : 256u;
+    int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
     parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 1024)));
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
-    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ent, pos, tab, mode, ps));
+    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ent, pos, tab, mode, lgC, ps));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
-    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ent, tab, sm, parts, s));
-    DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, s));
+    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ent, tab, sm, parts, lgC, s));
+    DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }
   return DLSM_OK;

@@ -56,8 +56,7 @@ struct LegacyJobDev {
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
 constexpr int kBuildChunk = 4096;   // keys per partition chunk (build)
-constexpr int kProbeChunk = 4096;   // keys per partition chunk (probe)
-constexpr int kProbeSliceLines = 128;  // 128 lines x 512 B stacked = 64 KiB LDS
+constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
 
 // ---- launchers (bloom_kernels.hip) -----------------------------------------
 // All return the hipError_t of the launch.  `dchunk` holds one
@@ -82,15 +81,16 @@ hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys,
                                int mode, hipStream_t s);
 hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, uint64_t* stacked,
                                 hipStream_t s);
+// lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice (7, 8).
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint16_t* tab, int mode, hipStream_t s);
+                                  uint16_t* tab, int mode, int lgC, hipStream_t s);
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
                                int lgR, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
-                               int parts, hipStream_t s);
+                               int parts, int lgC, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
-                                  uint8_t* mask, hipStream_t s);
+                                  uint8_t* mask, int lgC, hipStream_t s);
 
 hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s, int n_jobs,
                                  uint64_t total_keys, int mode, hipStream_t s);

@@ -23,6 +23,7 @@
 //   legacy CreateFilter      util/bloom.cc:25-55, KeyMayMatch :57-81
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "bloom_internal.h"
@@ -143,6 +144,17 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, int n, uint32_t* wsum) {
   }
   __syncthreads();
   return total;
+}
+
+// XCD-aware block order.  Workgroups are dispatched to the 8 XCDs
+// round-robin (block b -> XCD b % 8; a speed assumption only, results never
+// depend on it).  Renumber so each XCD gets one contiguous run of work items:
+// adjacent slices read adjacent bucket segments of every chunk (and write
+// adjacent answer bytes), so running them on one XCD turns the cache lines
+// they share into L2 hits / whole-line writes instead of one fetch per XCD.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t n) {
+  const uint32_t x = b & 7u, j = b >> 3, q = n >> 3, r = n & 7u;
+  return x * q + min(x, r) + j;
 }
 
 // Largest j with starts[j] <= b (starts non-decreasing, starts[0] == 0).
@@ -310,50 +322,66 @@ __device__ __forceinline__ uint32_t chunk_distinct(const uint32_t (&h)[PER], uin
   return tot;
 }
 
-// Inclusive max-scan over the wave in DPP: row_shr 1/2/4/8 inside each
-// 16-lane row, then row_bcast:15 / row_bcast:31 across rows (no LDS traffic).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+// Inclusive add-scan over the wave in DPP: row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast:15 / row_bcast:31 across rows (lanes outside a
+// step's source read 0; no LDS traffic).
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
   return v;
 }
 
-constexpr uint32_t kWin = 63;  // entries per walk window (lane 63 is the permute sink)
+constexpr uint32_t kWin = 64;  // entries per walk window (one per lane)
+
+// A wave-uniform 64-bit value moved to SGPRs (lets the compiler keep the
+// segment-boundary loop scalar: s_ff1 / s_flbit instead of per-lane loops).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x >> 32)));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
 
 // Segment walk over one group of up to 64 chunks.  Lane l holds segment l:
-// its flat range [excl, incl) inside the group (wave prefix scan of the
-// counts) and its marker dv = l*CHUNK + off - excl + 1, where off is the
-// segment's offset inside chunk l's region; entry e of segment l then sits at
-// in-group offset e + dv - 1, and dv is non-decreasing over the non-empty
-// segments.  For U windows of 63 entries (window u = [w0 + 63u, +63)), each
-// non-empty segment forward-permutes (ds_permute) its marker to the lane where
-// it starts in the window -- lane 0 for the one segment holding the window's
-// first entry -- and every other segment to lane 63, which is never read.  At
-// most one segment lands on each of lanes 0..62, so the result does not
-// depend on how the permute resolves collisions; an inclusive max-scan then
-// hands each lane the marker of its own segment.  One permute + 6 DPP steps
-// per window instead of a 6-step binary search.  Lanes past T (or lane 63)
-// get the window's first entry, so every index stays inside the group.
+// its flat start `excl` inside the group (wave prefix scan of the counts) and
+// dv = l*CHUNK + off - excl, where off is the segment's offset inside chunk
+// l's region, so flat entry e of segment l sits at in-group offset e + dv.
+// `nz` is the wave mask of non-empty segments.  A window [w, w+64) starts in
+// the last non-empty segment with excl <= w and crosses into every non-empty
+// segment that starts inside it; those boundaries are wave-uniform (ballot,
+// s_ff1, readlane), so each lane picks its dv with one compare + select per
+// boundary (about two per window at the bench shapes): no LDS permutes and
+// no per-window scans.  Lanes past T take the window's first entry, so every
+// index stays inside the group.
 template <int U>
-__device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t incl, uint32_t dv,
-                                               uint32_t T, uint32_t w0, uint32_t (&idx)[U],
-                                               bool (&ok)[U]) {
+__device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint64_t nz, uint32_t T,
+                                               uint32_t w0, uint32_t (&idx)[U], bool (&ok)[U]) {
   const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t w = w0 + u * kWin;
-    uint32_t dst = 63u;
-    if (excl <= w && w < incl) dst = 0u;
-    else if (excl > w && excl < incl && excl - w < kWin) dst = excl - w;
-    const uint32_t m = static_cast<uint32_t>(
-        __builtin_amdgcn_ds_permute(static_cast<int>(dst * 4u), static_cast<int>(dv)));
-    const uint32_t id = w + lane + wave_incl_max(m) - 1u;
-    const uint32_t id0 = w < T ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0)) : 0u;
-    ok[u] = lane < kWin && w + lane < T;
+    if (w >= T) {  // wave-uniform
+      ok[u] = false;
+      idx[u] = lane;
+      continue;
+    }
+    const uint64_t below = uniform64(__ballot(excl <= w) & nz);
+    uint32_t d = static_cast<uint32_t>(
+        __builtin_amdgcn_readlane(static_cast<int>(dv), 63 - __builtin_clzll(below)));
+    uint64_t m = uniform64(__ballot(excl > w && excl < w + kWin) & nz);
+    while (m) {
+      const int l = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t st = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(excl), l));
+      const uint32_t dl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dv), l));
+      if (w + lane >= st) d = dl;
+    }
+    const uint32_t id = w + lane + d;
+    const uint32_t id0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0));
+    ok[u] = w + lane < T;
     idx[u] = ok[u] ? id : id0;
   }
 }
@@ -373,7 +401,8 @@ struct SegWalk {
   uint32_t rowlen, g_step, g_end;
   uint32_t g;         // current group (first chunk)
   uint32_t e0;        // next window start in the current group
-  uint32_t excl, incl, dv, T;
+  uint32_t excl, dv, T;
+  uint64_t nz;        // non-empty segments of the current group
   uint32_t n0, n1;    // prefetched table row of group g + g_step (this lane's chunk)
 
   __device__ __forceinline__ void load_rows(uint32_t gg, uint32_t& a0, uint32_t& a1) const {
@@ -386,10 +415,11 @@ struct SegWalk {
   __device__ __forceinline__ void setup(uint32_t a0, uint32_t a1) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t cnt = g + lane < g_end ? a1 - a0 : 0u;
-    incl = wave_incl_scan(cnt);
+    const uint32_t incl = wave_incl_scan_dpp(cnt);
     excl = incl - cnt;
-    T = __shfl(incl, 63, 64);
-    dv = lane * CHUNK + a0 - excl + 1u;
+    T = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    dv = lane * CHUNK + a0 - excl;
+    nz = uniform64(__ballot(cnt != 0u));
     e0 = 0;
   }
   __device__ __forceinline__ bool start(uint32_t g_first) {
@@ -410,7 +440,7 @@ struct SegWalk {
       if (g + g_step < g_end) load_rows(g + g_step, n0, n1);
       setup(a0, a1);
     }
-    seg_locate_win<U>(excl, incl, dv, T, e0, idx, ok);
+    seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
     e0 += kWin * U;
     gset = g;
     return true;
@@ -573,7 +603,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
   __shared__ uint32_t wsum[NW];
   __shared__ int sj;
   const int tid = threadIdx.x, wv = tid >> 6;
-  const uint32_t bid = blockIdx.x + block0;  // slice index over all jobs
+  const uint32_t bid = xcd_block(blockIdx.x, gridDim.x) + block0;  // slice index over all jobs
   if (tid == 0) sj = find_job(slice0s, n_jobs, bid);
   for (uint32_t w = tid; w < R * 16; w += kSliceBlock) sl[w] = 0;
   __syncthreads();
@@ -753,61 +783,65 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
 
 // Pass 1: hash each lookup once and bucket it by slice inside its chunk.
 // entries[chunk region] = hashes grouped by slice; pos[i] = where key i went.
-template <int MODE>
-__global__ __launch_bounds__(kPartBlock) void probe_partition_kernel(
+// NT threads per chunk of C keys (C/NT keys per thread).
+template <int MODE, int NT, int C>
+__global__ __launch_bounds__(NT) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
-  constexpr int C = kProbeChunk;
-  constexpr int PER = C / kPartBlock;
-  constexpr int TV = K20Tile<kPartBlock, kTileKPT>::kVec;
-  static_assert(TV * 16 >= C * 4, "the key tile doubles as the bucketed-hash staging area");
+  constexpr int PER = C / NT;
+  // the key tile doubles as the bucketed-hash staging area (C u32)
+  constexpr int TV = K20Tile<NT, kTileKPT>::kVec > C / 4 ? K20Tile<NT, kTileKPT>::kVec : C / 4;
+  static_assert(PER % kTileKPT == 0 && C <= 65536, "chunk shape");
   __shared__ __attribute__((aligned(16))) uint4 tile[TV];
   __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
   __shared__ uint8_t sb[C];                                // slice (S <= 256)
   __shared__ uint32_t hist[kMaxSlices + 1];
-  __shared__ uint32_t wsum[kPartBlock / 64];
+  __shared__ uint32_t wsum[NT / 64];
   const int tid = threadIdx.x;
-  const uint32_t c = blockIdx.x;
-  const uint64_t first = static_cast<uint64_t>(c) * C;
-  const uint64_t left = kd.n - first;
-  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
-  for (uint32_t b = tid; b <= S; b += kPartBlock) hist[b] = 0;
-  uint32_t h[PER];
-  hash_chunk<MODE, kPartBlock, PER>(kd, first, nk, tile, h);  // ends with a barrier
+  // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
+  for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
+    const uint64_t first = static_cast<uint64_t>(c) * C;
+    const uint64_t left = kd.n - first;
+    const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+    for (uint32_t b = tid; b <= S; b += NT) hist[b] = 0;
+    uint32_t h[PER];
+    hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);  // ends with a barrier
 #pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kPartBlock + tid;
-    if (i < nk) {
-      const uint32_t sl = fastmod(h[r], L, magic) >> lgR;
-      sb[i] = static_cast<uint8_t>(sl);
-      rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + tid;
+      if (i < nk) {
+        const uint32_t sl = fastmod(h[r], L, magic) >> lgR;
+        sb[i] = static_cast<uint8_t>(sl);
+        rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+      }
     }
-  }
-  __syncthreads();
-  block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
-  for (uint32_t b = tid; b <= S; b += kPartBlock)
-    tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);  // one row per chunk
-  uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
+    __syncthreads();
+    block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
+    for (uint32_t b = tid; b <= S; b += NT)
+      tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);  // one row per chunk
+    uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
 #pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const uint32_t i = r * kPartBlock + tid;
-    if (i < nk) {
-      const uint32_t p = hist[sb[i]] + rk[i];
-      stage[p] = h[r];
-      rk[i] = static_cast<uint16_t>(p);
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + tid;
+      if (i < nk) {
+        const uint32_t p = hist[sb[i]] + rk[i];
+        stage[p] = h[r];
+        rk[i] = static_cast<uint16_t>(p);
+      }
     }
+    __syncthreads();
+    // coalesced 16-byte stores of the bucketed hashes and of the positions
+    store_chunk_u32<NT>(entries + first, stage, nk);
+    store_chunk_u16<NT>(pos + first, rk, nk);
+    __syncthreads();  // LDS reused by the next chunk
   }
-  __syncthreads();
-  // coalesced 16-byte stores of the bucketed hashes and of the positions
-  store_chunk_u32<kPartBlock>(entries + first, stage, nk);
-  store_chunk_u16<kPartBlock>(pos + first, rk, nk);
 }
 
 // Pass 2: one NT-thread workgroup per (slice of 2^LGR stacked lines, part of
-// the chunks); the slice (64 KiB) sits in LDS, waves walk the slice's
+// the chunks of C keys); the slice (R x 512 B: 64 or 128 KiB) sits in LDS, waves walk the slice's
 // segments of 64 chunks at a time, 6 windows of 63 hashes in flight per wave.
 // smask gets each key's F-bit answer at the key's bucketed position.
-template <int LGR, int K, int NT>
+template <int LGR, int K, int NT, int C>
 __global__ __launch_bounds__(NT) void probe_slice_kernel(
     const uint8_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
@@ -817,8 +851,9 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
   const int tid = threadIdx.x, wv = tid >> 6;
-  const uint32_t s = blockIdx.x % S;
-  const uint32_t p = blockIdx.x / S;
+  const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
+  const uint32_t s = wi % S;
+  const uint32_t p = wi / S;
   const uint32_t lo_line = s << LGR;
   const uint32_t nl = min(R, L - lo_line);
   {
@@ -838,10 +873,10 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
   __syncthreads();
-  walk_segments<U, kProbeChunk>(
+  walk_segments<U, C>(
       tb, S + 1, entries, c_lo + wv * 64u, NW * 64u, c_hi,
       [&](const uint32_t (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
-        uint8_t* gmask = smask + static_cast<uint64_t>(g) * kProbeChunk;
+        uint8_t* gmask = smask + static_cast<uint64_t>(g) * C;
 #pragma unroll
         for (int u = 0; u < U; u++) {
           // per-hash branch: keeps each hash's k LDS reads the only ones live
@@ -874,11 +909,11 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
 // (16-byte loads), gather them back to key order through pos (16-byte loads
 // of 8 positions), store 8 answers per lane.
+template <int C>
 __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
                                                                  const uint16_t* __restrict__ pos,
                                                                  const uint8_t* __restrict__ smask,
                                                                  uint8_t* __restrict__ mask) {
-  constexpr int C = kProbeChunk;
   __shared__ __attribute__((aligned(16))) uint8_t sm[C];
   const int tid = threadIdx.x;
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * C;
@@ -1058,49 +1093,98 @@ hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, 
   return hipGetLastError();
 }
 
+// Compute units of the current device (cached per device id).
+static uint32_t device_cus() {
+  static uint32_t cus[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256u;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = static_cast<uint32_t>(n);
+  }
+  return cus[dev];
+}
+
+// Probe chunk shapes: C keys per partition workgroup of NT threads.
+//   lgC 12: C = 4096, 512 threads;  13: 8192, 1024;  14: 16384, 1024.
+template <int C, int NT>
+static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
+                                     uint32_t n_slices, uint32_t* entries, uint16_t* pos,
+                                     uint16_t* tab, int mode, hipStream_t s) {
+  const uint32_t nC = static_cast<uint32_t>((keys.n + C - 1) / C);
+  if (nC == 0) return hipSuccess;
+  // persistent: a few resident workgroups per CU loop over the chunks
+  // ($DLSM_PART_GRID_PER_CU, default 2; 0 = one workgroup per chunk)
+  static const uint32_t per_cu = [] {
+    const char* e = getenv("DLSM_PART_GRID_PER_CU");
+    return e ? static_cast<uint32_t>(atoi(e)) : 2u;
+  }();
+  const uint32_t g = per_cu ? std::min(nC, per_cu * device_cus()) : nC;
+  if (mode == KM_K20)
+    probe_partition_kernel<KM_K20, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+                                                          entries, pos, tab);
+  else
+    probe_partition_kernel<KM_GENERIC, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+                                                              entries, pos, tab);
+  return hipGetLastError();
+}
+
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint16_t* tab, int mode, hipStream_t s) {
-  const uint32_t nC = static_cast<uint32_t>((keys.n + kProbeChunk - 1) / kProbeChunk);
-  if (nC == 0) return hipSuccess;
-  if (mode == KM_K20)
-    probe_partition_kernel<KM_K20><<<nC, kPartBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
-                                                         entries, pos, tab);
+                                  uint16_t* tab, int mode, int lgC, hipStream_t s) {
+  switch (lgC) {
+    case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 14: return probe_partition_as<16384, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int LGR, int C>
+static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
+                                  uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
+                                  const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
+  const uint8_t* st = reinterpret_cast<const uint8_t*>(stacked);
+  if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
+    probe_slice_kernel<LGR, 6, 1024, C><<<n_slices * parts, 1024, 0, s>>>(
+        st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
   else
-    probe_partition_kernel<KM_GENERIC><<<nC, kPartBlock, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
-                                                             entries, pos, tab);
+    probe_slice_kernel<LGR, 0, 1024, C><<<n_slices * parts, 1024, 0, s>>>(
+        st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR,
                                uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
-                               const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
+                               const uint16_t* tab, uint8_t* smask, int parts, int lgC,
+                               hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
-  if (lgR != 7) return hipErrorInvalidValue;
-  static const int nt = [] {
-    const char* e = getenv("DLSM_PROBE_SLICE_THREADS");
-    return e && atoi(e) == 512 ? 512 : 1024;
-  }();
-#define DLSM_PROBE_SLICE(KK, NTT)                                                        \
-  probe_slice_kernel<7, KK, NTT><<<n_slices * parts, NTT, 0, s>>>(                        \
-      reinterpret_cast<const uint8_t*>(stacked), L, magic, k, n_slices, n_chunks, entries, \
-      tab, smask, parts)
-  if (k == 6) {  // bits_per_key 10 (ChooseNumProbes)
-    if (nt == 512) DLSM_PROBE_SLICE(6, 512);
-    else DLSM_PROBE_SLICE(6, 1024);
-  } else {
-    if (nt == 512) DLSM_PROBE_SLICE(0, 512);
-    else DLSM_PROBE_SLICE(0, 1024);
+#define DLSM_SLICES(LG, CC) \
+  return probe_slices_as<LG, CC>(stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts, s)
+  if (lgR == 7) {
+    if (lgC == 12) DLSM_SLICES(7, 4096);
+    if (lgC == 13) DLSM_SLICES(7, 8192);
+    if (lgC == 14) DLSM_SLICES(7, 16384);
+  } else if (lgR == 8) {
+    if (lgC == 12) DLSM_SLICES(8, 4096);
+    if (lgC == 13) DLSM_SLICES(8, 8192);
+    if (lgC == 14) DLSM_SLICES(8, 16384);
   }
-#undef DLSM_PROBE_SLICE
-  return hipGetLastError();
+#undef DLSM_SLICES
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
-                                  uint8_t* mask, hipStream_t s) {
+                                  uint8_t* mask, int lgC, hipStream_t s) {
   if (n_keys == 0) return hipSuccess;
-  const uint64_t nC = (n_keys + kProbeChunk - 1) / kProbeChunk;
-  probe_unpermute_kernel<<<static_cast<unsigned>(nC), kBlock, 0, s>>>(n_keys, pos, smask, mask);
+  const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
+  switch (lgC) {
+    case 12: probe_unpermute_kernel<4096><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
+    case 13: probe_unpermute_kernel<8192><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
+    case 14: probe_unpermute_kernel<16384><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -1,8 +1,9 @@
 #!/usr/bin/env bash
-# One measuring GPU session: parity tests, the full bench line (cpu_baseline +
-# e2e), a rocprofv3 kernel-trace summary, then PMC passes (one counter group
-# per run, --kernel-trace only).  Each GPU step has its own time limit; the
-# steps are chained with && so the first failure ends the session.
+# One measuring GPU session: parity tests, rocprofv3 PMC passes (one counter
+# group per run, --kernel-trace only) -> per-launch traffic summary, the full
+# bench line (cpu_baseline + e2e + traffic), and a rocprofv3 kernel-trace
+# --stats summary of the same bench command.  Each GPU step has its own time
+# limit; the steps are chained with && so the first failure ends the session.
 #   scripts/gpu_measure.sh OUTDIR [extra bench args...]
 set -o pipefail
 OUT=${1:-gpurun_out/measure}
@@ -12,14 +13,18 @@ export TMPDIR=/tmp
 BARGS="$*"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > "$OUT/pytest_gpu.log" 2>&1 &&
-timeout -k 10 400 python bench.py $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e $BARGS > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
+timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 i=0 &&
 for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_ANY TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc$i" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $BARGS > "$OUT/pmc$i.json" 2> "$OUT/pmc$i.err" || exit 1
-done
+  mkdir -p "$OUT/pmc" &&
+  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $BARGS > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
+done &&
+python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" > /dev/null &&
+timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --traffic "$OUT/traffic.json" $BARGS \
+  > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err"

@@ -234,8 +234,38 @@ def test_full_probe_pipelined_rounds(gpu, orc, round_keys):
         gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
         gpu.sync()
     finally:
-        gpu.set_probe_round(4 << 20)
+        gpu.set_probe_round(0)
     assert np.array_equal(mask.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("chunk_lg", [12, 13, 14])
+@pytest.mark.parametrize("slice_lg", [7, 8])
+def test_full_probe_shapes(gpu, orc, chunk_lg, slice_lg):
+    """Every sliced-probe shape (chunk of 4096/8192/16384 keys x 64/128 KiB
+    LDS slices) gives the oracle's masks: a ragged key count, filters whose
+    line count is not a multiple of the slice, and a 60-line filter set
+    (one partial slice)."""
+    import torch
+
+    import dlsm_amd
+
+    for n_per, nq in ((100_000, 300_007), (3_000, 20_001)):
+        filters = [orc.full_build(orc.dbbench_keys(f, 8, n_per), n_per) for f in range(8)]
+        q = orc.keys_from_values(orc.mt_values(91 + chunk_lg, 8 * n_per * 2, nq))
+        want = orc.full_probe(filters, q, nq, nthreads=8)
+        fs = gpu.filterset(filters)
+        qd = torch.from_numpy(q).cuda()
+        mask = torch.full((nq,), 0xEE, dtype=torch.uint8, device="cuda")
+        gpu.set_path(2)
+        gpu.set_probe_shape(chunk_lg, slice_lg)
+        try:
+            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
+            gpu.sync()
+        finally:
+            gpu.set_probe_shape(13, 7)
+            gpu.set_path(0)
+        fs.close()
+        assert np.array_equal(mask.cpu().numpy(), want), (n_per, nq)
 
 
 @pytest.mark.parametrize("groups", [1, 2, 3, 4])
@@ -277,6 +307,10 @@ def test_set_option_rejects_bad_values(gpu):
         gpu.set_option(99, 1)
     with pytest.raises(dlsm_amd.DlsmError):
         gpu.set_option(dlsm_amd.OPT_PATH, 3)
+    for opt, bad in ((dlsm_amd.OPT_PROBE_CHUNK_LG, 11), (dlsm_amd.OPT_PROBE_CHUNK_LG, 15),
+                     (dlsm_amd.OPT_PROBE_SLICE_LG, 6), (dlsm_amd.OPT_PROBE_SLICE_LG, 9)):
+        with pytest.raises(dlsm_amd.DlsmError):
+            gpu.set_option(opt, bad)
 
 
 def test_full_probe_many_filters_and_varlen(gpu, orc):
