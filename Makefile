@@ -30,8 +30,15 @@ asm: dlsm_amd/csrc/bloom_kernels.hip $(HDR)
 	$(HIPCC) $(HIPFLAGS) --offload-device-only -S $< -o build/asm/bloom_kernels.s \
 	  -Rpass-analysis=kernel-resource-usage 2> build/asm/resource_usage.txt || true
 
+# A/B build with extra defines: make variant TAG=u4 VFLAGS="-DDLSM_PROBE_U=4"
+# -> dlsm_amd/lib/variants/libdlsm_bloom_u4.so (loaded with DLSM_LIB_VARIANT=u4)
+variant: $(SRC) $(HDR)
+	@mkdir -p build/variants/$(TAG) dlsm_amd/lib/variants
+	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) $(VFLAGS) -c $$f -o build/variants/$(TAG)/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC build/variants/$(TAG)/*.o -o dlsm_amd/lib/variants/libdlsm_bloom_$(TAG).so
+
 clean:
 	rm -rf build dlsm_amd/lib
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle oracle-ref asm clean
+.PHONY: all oracle oracle-ref asm variant clean

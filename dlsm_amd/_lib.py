@@ -11,6 +11,11 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libdlsm_bloom.so")
+# A/B tuning only: $DLSM_LIB_VARIANT=<tag> loads the in-tree build
+# dlsm_amd/lib/variants/libdlsm_bloom_<tag>.so (``make variant``) instead.
+if os.environ.get("DLSM_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_HERE, "lib", "variants",
+                            f"libdlsm_bloom_{os.environ['DLSM_LIB_VARIANT']}.so")
 
 DLSM_OK = 0
 DLSM_E_ARG = -1

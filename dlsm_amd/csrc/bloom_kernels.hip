@@ -337,6 +337,13 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 
 constexpr uint32_t kWin = 64;  // entries per walk window (one per lane)
 
+// The wave's index in its workgroup as a wave-uniform (SGPR) value: derived
+// from threadIdx.x the compiler would treat it, and every walk counter built
+// from it, as divergent (exec-mask loops, vmcnt(0) waits on prefetches).
+__device__ __forceinline__ int wave_id() {
+  return __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+}
+
 // A wave-uniform 64-bit value moved to SGPRs (lets the compiler keep the
 // segment-boundary loop scalar: s_ff1 / s_flbit instead of per-lane loops).
 __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
@@ -589,7 +596,13 @@ __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint
 constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
 // probe slices: 64 KiB LDS per workgroup, 512 or 1024 threads (launch_probe_slices)
 constexpr int kWalkU = 8;               // hashes in flight per lane (build segment walk)
-constexpr int kProbeWalkU = 6;          // probe walk: 6 keeps 2 x 1024-thread groups per CU (<= 64 VGPRs)
+#ifndef DLSM_PROBE_U
+#define DLSM_PROBE_U 4
+#endif
+#ifndef DLSM_PROBE_MINWAVES
+#define DLSM_PROBE_MINWAVES 1
+#endif
+constexpr int kProbeWalkU = DLSM_PROBE_U;  // probe walk: windows (hashes per lane) in flight
 
 template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
@@ -602,7 +615,8 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
   __shared__ int sj;
-  const int tid = threadIdx.x, wv = tid >> 6;
+  const int tid = threadIdx.x;
+  const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t bid = xcd_block(blockIdx.x, gridDim.x) + block0;  // slice index over all jobs
   if (tid == 0) sj = find_job(slice0s, n_jobs, bid);
   for (uint32_t w = tid; w < R * 16; w += kSliceBlock) sl[w] = 0;
@@ -781,8 +795,21 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
   }
 }
 
+// A probe only reads hash bits [0, 9) (first bit position) and [17, 26)
+// (the low 9 bits of delta = rotr(h, 17)): HashMayMatchPrepared,
+// util/bloom_impl.h:466-479, with every position taken mod 512.  The
+// partition therefore parks the key's line offset inside its slice (< 256)
+// in the unused bits [9, 17), so the slice pass needs no modulo: the LDS base
+// of the key's line is `e & kEntryLineMask` (= offset * 512) and the
+// positions are (e + q * (e >> 17)) & 511, exactly those of h.
+constexpr uint32_t kEntryLineMask = 0xffu << 9;
+__device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
+  return (h & ~kEntryLineMask) | (line_off << 9);
+}
+
 // Pass 1: hash each lookup once and bucket it by slice inside its chunk.
-// entries[chunk region] = hashes grouped by slice; pos[i] = where key i went.
+// entries[chunk region] = packed entries (probe_entry) grouped by slice;
+// pos[i] = where key i went.
 // NT threads per chunk of C keys (C/NT keys per thread).
 template <int MODE, int NT, int C>
 __global__ __launch_bounds__(NT) void probe_partition_kernel(
@@ -810,9 +837,11 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
     for (int r = 0; r < PER; r++) {
       const uint32_t i = r * NT + tid;
       if (i < nk) {
-        const uint32_t sl = fastmod(h[r], L, magic) >> lgR;
+        const uint32_t line = fastmod(h[r], L, magic);
+        const uint32_t sl = line >> lgR;
         sb[i] = static_cast<uint8_t>(sl);
         rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+        h[r] = probe_entry(h[r], line & ((1u << lgR) - 1u));
       }
     }
     __syncthreads();
@@ -842,7 +871,7 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
 // segments of 64 chunks at a time, 6 windows of 63 hashes in flight per wave.
 // smask gets each key's F-bit answer at the key's bucketed position.
 template <int LGR, int K, int NT, int C>
-__global__ __launch_bounds__(NT) void probe_slice_kernel(
+__global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     const uint8_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
@@ -850,7 +879,8 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
   constexpr int U = kProbeWalkU;
   constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
-  const int tid = threadIdx.x, wv = tid >> 6;
+  const int tid = threadIdx.x;
+  const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
   const uint32_t s = wi % S;
   const uint32_t p = wi / S;
@@ -877,32 +907,32 @@ __global__ __launch_bounds__(NT) void probe_slice_kernel(
       tb, S + 1, entries, c_lo + wv * 64u, NW * 64u, c_hi,
       [&](const uint32_t (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint8_t* gmask = smask + static_cast<uint64_t>(g) * C;
+        // straight-line over the U hashes (no per-hash branch), so the
+        // compiler can keep several hashes' LDS reads in flight; lanes without
+        // an entry probe a harmless in-slice address and store nothing
+        uint32_t acc[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-          // per-hash branch: keeps each hash's k LDS reads the only ones live
-          if (!ok[u]) continue;
           uint32_t x = hv[u];
-          const uint32_t base = (fastmod(x, L, magic) - lo_line) << 9;  // 512 stacked bytes per line
-          const uint32_t delta = bloom_delta(x);
-          uint32_t acc = 0xffu;
+          const uint32_t base = x & ((R - 1u) << 9);  // line offset * 512 stacked bytes (probe_entry)
+          const uint32_t delta = x >> 17;            // low 9 bits of rotr(h, 17)
+          acc[u] = 0xffu;
           if constexpr (K > 0) {
-            // k known at compile time: all k LDS reads issue back to back
-            uint32_t v[K];
 #pragma unroll
             for (int q = 0; q < K; q++) {
-              v[q] = sl[base | (x & 511u)];
+              acc[u] &= sl[base | (x & 511u)];
               x += delta;
             }
-#pragma unroll
-            for (int q = 0; q < K; q++) acc &= v[q];
           } else {
             for (int q = 0; q < k; q++) {
-              acc &= sl[base | (x & 511u)];
+              acc[u] &= sl[base | (x & 511u)];
               x += delta;
             }
           }
-          gmask[idx[u]] = static_cast<uint8_t>(acc);
         }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (ok[u]) gmask[idx[u]] = static_cast<uint8_t>(acc[u]);
       });
 }
 
