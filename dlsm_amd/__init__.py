@@ -31,6 +31,8 @@ __all__ = [
 ]
 
 PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
+INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbformat.h:374-377)
+SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG = 3, 4
 
@@ -103,9 +105,10 @@ class Keys:
     n: int
     key_len: int = 20
     offsets: object = None
+    suffix_len: int = 0  # INTERNAL_KEY_TRAILER: internal keys, hashed as ExtractUserKey(key)
 
     def c(self) -> dlsm_keyset:
-        return dlsm_keyset(_ptr(self.data), _ptr(self.offsets), self.key_len, 0, self.n)
+        return dlsm_keyset(_ptr(self.data), _ptr(self.offsets), self.key_len, self.suffix_len, self.n)
 
     @staticmethod
     def pack(keys: Sequence[bytes]) -> "Keys":
@@ -267,6 +270,26 @@ class Context:
         out = (C.c_uint32 * max(n, 1))()
         check(lib().dlsm_crc32c_dev(self.h, ptrs, lens, n, out), "crc32c_dev")
         return [int(out[j]) for j in range(n)]
+
+    # -- internal keys: flush / compaction selection, user-key gather --------
+    def internal_keys_select_dev(self, keys: Keys, policy: int, smallest_snapshot: int, keep):
+        """keep (device uint8[n]) <- 1 for every key the flush / compaction loop
+        passes to TableBuilder::Add.  Returns (n_kept, kept_user_key_bytes,
+        first_corrupt or None).  A flush over a corrupt key raises DlsmError
+        (DLSM_E_CORRUPT) like the reference's IOError."""
+        ks = keys.c()
+        nk, nb, bad = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        st = lib().dlsm_internal_keys_select_dev(self.h, C.byref(ks), policy, smallest_snapshot,
+                                                 _ptr(keep), C.byref(nk), C.byref(nb), C.byref(bad))
+        check(st, "internal_keys_select_dev")
+        return int(nk.value), int(nb.value), (None if bad.value == 2**64 - 1 else int(bad.value))
+
+    def user_keys_gather_dev(self, keys: Keys, keep, out, offsets=None):
+        """Pack ExtractUserKey(key) of the kept keys into `out` (device uint8);
+        variable-length keys also fill `offsets` (device uint64[n_kept+1])."""
+        ks = keys.c()
+        check(lib().dlsm_user_keys_gather_dev(self.h, C.byref(ks), _ptr(keep), _ptr(out), _ptr(offsets)),
+              "user_keys_gather_dev")
 
     # -- full filter probe --------------------------------------------------
     def filterset(self, filters, on_device: bool = False) -> FilterSet:

@@ -27,7 +27,7 @@ DLSM_E_NOMEM = -5
 
 class dlsm_keyset(C.Structure):
     _fields_ = [("bytes", C.c_void_p), ("offsets", C.c_void_p), ("key_len", C.c_uint32),
-                ("reserved", C.c_uint32), ("n", C.c_uint64)]
+                ("suffix_len", C.c_uint32), ("n", C.c_uint64)]
 
 
 class dlsm_build_job(C.Structure):
@@ -76,6 +76,9 @@ SIGNATURES = [
     ("dlsm_filterset_destroy", C.c_int, [_VP]),
     ("dlsm_filterset_size", C.c_int, [_VP, C.POINTER(C.c_int), _U64P]),
     ("dlsm_bloom_full_probe_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_internal_keys_select_dev", C.c_int, [_VP, C.POINTER(dlsm_keyset), C.c_int, C.c_uint64,
+                                                _VP, _U64P, _U64P, _U64P]),
+    ("dlsm_user_keys_gather_dev", C.c_int, [_VP, C.POINTER(dlsm_keyset), _VP, _VP, _VP]),
     ("dlsm_bloom_full_probe", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_legacy_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),

@@ -120,6 +120,8 @@ struct dlsm_ctx {
   DevBuf<uint8_t*> crc_outp;
   DevBuf<uint64_t> crc_cap;
   DevBuf<uint32_t> crc_val;
+  // internal-key selection / gather: [blk_cnt | blk_bytes | tot(2) | first_bad]
+  DevBuf<uint64_t> sel;
 };
 
 struct dlsm_filterset {
@@ -151,10 +153,9 @@ struct DeviceGuard {
 int validate_keyset(const dlsm_keyset& k) {
   if (k.n == 0) return DLSM_OK;
   if (!k.bytes) return DLSM_E_ARG;
-  if (!k.offsets && k.key_len == 0) {
-    // zero-length fixed keys are legal (every key is the empty string)
-    return DLSM_OK;
-  }
+  if (k.suffix_len > 255) return DLSM_E_ARG;
+  // fixed keys must hold the stripped suffix; zero-length user keys are legal
+  if (!k.offsets && k.key_len < k.suffix_len) return DLSM_E_ARG;
   return DLSM_OK;
 }
 
@@ -164,13 +165,14 @@ KeyDesc to_desc(const dlsm_keyset& k) {
   d.offsets = k.offsets;
   d.n = k.n;
   d.key_len = k.key_len;
-  d.pad = 0;
+  d.suffix = k.suffix_len;
   return d;
 }
 
 // The K20 kernels stage keys through LDS with 16-byte loads.
 bool is_k20(const dlsm_keyset& k) {
-  return k.offsets == nullptr && k.key_len == 20 && (k.n == 0 || aligned(k.bytes, 16));
+  return k.offsets == nullptr && k.key_len == 20 && k.suffix_len == 0 &&
+         (k.n == 0 || aligned(k.bytes, 16));
 }
 
 // Slice width for the sliced build: the smallest 2^lgR (lgR in [9, 11]) that
@@ -327,6 +329,7 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->lstarts.release();
   ctx->pos.release();
   ctx->smask.release();
+  ctx->sel.release();
   ctx->st_keys.release();
   ctx->st_offs.release();
   ctx->st_out.release();
@@ -742,6 +745,64 @@ int dlsm_crc32c_dev(dlsm_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
   DLSM_CHECK(run_crc(ctx, st, n, max_total, nullptr, nullptr, nullptr, ctx->crc_val.p));
   DLSM_TRY(hipMemcpyAsync(crc_out, ctx->crc_val.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
   DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  return DLSM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Internal keys: flush / compaction selection and user-key gather
+// ---------------------------------------------------------------------------
+int dlsm_internal_keys_select_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, int policy,
+                                  uint64_t smallest_snapshot, uint8_t* keep_dev, uint64_t* n_kept,
+                                  uint64_t* kept_bytes, uint64_t* first_corrupt) {
+  if (!ctx || !ikeys || (policy != DLSM_SELECT_FLUSH && policy != DLSM_SELECT_COMPACTION))
+    return DLSM_E_ARG;
+  dlsm_keyset k = *ikeys;
+  k.suffix_len = 0;
+  DLSM_CHECK(validate_keyset(k));
+  if (ikeys->n > 0 && !keep_dev) return DLSM_E_ARG;
+  uint64_t res[4] = {0, 0, ~uint64_t(0), 0};  // n_kept, kept_bytes, first_bad
+  if (k.n > 0) {
+    DeviceGuard g(ctx->device);
+    hipStream_t s = ctx->stream;
+    const uint64_t nb = select_blocks(k.n);
+    DLSM_CHECK(ctx->sel.ensure(2 * nb + 3));
+    uint64_t* bc = ctx->sel.p;
+    uint64_t* bb = bc + nb;
+    uint64_t* tot = bb + nb;
+    uint64_t* bad = tot + 2;
+    DLSM_TRY(hipMemsetAsync(bad, 0xff, sizeof(uint64_t), s));
+    DLSM_TRY(launch_key_select(to_desc(k), policy, smallest_snapshot, keep_dev, bc, bb,
+                               reinterpret_cast<unsigned long long*>(bad), tot, s));
+    DLSM_TRY(hipMemcpyAsync(res, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    DLSM_TRY(hipStreamSynchronize(s));
+  }
+  if (n_kept) *n_kept = res[0];
+  if (kept_bytes) *kept_bytes = res[1];
+  if (first_corrupt) *first_corrupt = res[2];
+  if (policy == DLSM_SELECT_FLUSH && res[2] != ~uint64_t(0)) return DLSM_E_CORRUPT;
+  return DLSM_OK;
+}
+
+int dlsm_user_keys_gather_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, const uint8_t* keep_dev,
+                              uint8_t* user_keys_dev, uint64_t* offsets_dev) {
+  if (!ctx || !ikeys) return DLSM_E_ARG;
+  dlsm_keyset k = *ikeys;
+  k.suffix_len = 0;
+  DLSM_CHECK(validate_keyset(k));
+  if (k.offsets && !offsets_dev) return DLSM_E_ARG;
+  if (!k.offsets && k.key_len < DLSM_INTERNAL_KEY_TRAILER) return DLSM_E_ARG;
+  if (k.n == 0) {
+    if (offsets_dev) DLSM_TRY(hipMemsetAsync(offsets_dev, 0, sizeof(uint64_t), ctx->stream));
+    return DLSM_OK;
+  }
+  if (!keep_dev || !user_keys_dev) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  const uint64_t nb = select_blocks(k.n);
+  DLSM_CHECK(ctx->sel.ensure(2 * nb + 3));
+  uint64_t* bc = ctx->sel.p;
+  uint64_t* bb = bc + nb;
+  DLSM_TRY(launch_key_gather(to_desc(k), keep_dev, bc, bb, user_keys_dev,
+                             k.offsets ? offsets_dev : nullptr, bb + nb, ctx->stream));
   return DLSM_OK;
 }
 

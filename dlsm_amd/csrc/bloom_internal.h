@@ -19,7 +19,7 @@ struct KeyDesc {
   const uint64_t* offsets;  // n+1 entries or nullptr
   uint64_t n;
   uint32_t key_len;
-  uint32_t pad;
+  uint32_t suffix;  // bytes dropped from each key's end before hashing (ExtractUserKey: 8)
 };
 
 // One full-filter build job as the kernels see it.
@@ -96,6 +96,16 @@ hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,
                                int trivial, KeyDesc keys, uint8_t* out, int mode, hipStream_t s);
+
+// key_select.hip: internal-key selection (flush / compaction drop rules) and
+// the packing of kept user keys.  Workspace: blk_cnt / blk_bytes hold
+// select_blocks(n) u64 each, tot 2 u64, first_bad 1 u64 (preset to ~0).
+uint64_t select_blocks(uint64_t n);
+hipError_t launch_key_select(KeyDesc kd, int mode, uint64_t snapshot, uint8_t* keep, uint64_t* blk_cnt,
+                             uint64_t* blk_bytes, unsigned long long* first_bad, uint64_t* tot,
+                             hipStream_t s);
+hipError_t launch_key_gather(KeyDesc kd, const uint8_t* keep, uint64_t* blk_cnt, uint64_t* blk_bytes,
+                             uint8_t* out, uint64_t* out_offsets, uint64_t* tot, hipStream_t s);
 
 // block_crc.hip: crc32c of device streams, optionally sealing filter blocks.
 uint64_t crc_max_parts(uint64_t max_len_plus_extra);

@@ -86,6 +86,7 @@ __device__ __forceinline__ uint32_t key_hash(const KeyDesc& kd, uint64_t i) {
       s = i * kd.key_len;
       l = kd.key_len;
     }
+    l = l > kd.suffix ? l - kd.suffix : 0;  // ExtractUserKey (db/dbformat.h:374-377)
     return hash_bytes(kd.bytes + s, l);
   }
 }

@@ -51,15 +51,22 @@ typedef struct dlsm_filterset dlsm_filterset; /* F parsed full filters resident 
 
 /* A packed key set.  Fixed-length keys: offsets == NULL and every key is
  * key_len bytes at bytes + i*key_len.  Variable-length keys: offsets has n+1
- * entries and key i is bytes[offsets[i], offsets[i+1]).  The reference hashes
- * user keys (ExtractUserKey, db/dbformat.h:374-377): callers strip the 8-byte
- * internal-key trailer before handing keys over, exactly as
- * table_builder_computeside.cc:222-224 does. */
+ * entries and key i is bytes[offsets[i], offsets[i+1]).
+ *
+ * The reference hashes user keys (ExtractUserKey, db/dbformat.h:374-377, as
+ * table_builder_computeside.cc:222-224 and InternalFilterPolicy,
+ * db/dbformat.cc:93-109, do).  suffix_len = 0: the keys are user keys, hashed
+ * as given.  suffix_len = DLSM_INTERNAL_KEY_TRAILER (8): the keys are internal
+ * keys (user key || Fixed64(sequence << 8 | type)) straight from a memtable or
+ * compaction iterator, and every build / probe hashes ExtractUserKey(key).
+ * Fixed-length keys need key_len >= suffix_len; a variable-length key shorter
+ * than suffix_len (the reference asserts) hashes as the empty user key. */
+#define DLSM_INTERNAL_KEY_TRAILER 8
 typedef struct {
   const uint8_t* bytes;
   const uint64_t* offsets;
   uint32_t key_len;
-  uint32_t reserved;
+  uint32_t suffix_len;
   uint64_t n;
 } dlsm_keyset;
 
@@ -169,6 +176,43 @@ int dlsm_crc32c_dev(dlsm_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
 /* Host helpers: crc32c::Extend and crc32c::Mask (util/crc32c.h:17-31). */
 uint32_t dlsm_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
 uint32_t dlsm_crc32c_mask(uint32_t crc);
+
+/* ---- internal keys: the flush / compaction loops that feed AddKey -------- */
+
+/* The two compute-node loops that hand keys to TableBuilder::Add (and so to
+ * FullFilterBlockBuilder::AddKey through ExtractUserKey):
+ *   DLSM_SELECT_FLUSH       FlushJob::BuildTable, db/memtable_list.cc:855-886:
+ *                           keep the first entry of each user key; a key that
+ *                           ParseInternalKey (db/dbformat.h:451-461) rejects
+ *                           aborts the flush (IOError).
+ *   DLSM_SELECT_COMPACTION  DBImpl::DoCompactionWork, db/db_impl.cc:3500-3562:
+ *                           drop an entry hidden by a newer one of the same user
+ *                           key whose sequence <= smallest_snapshot (rule (A));
+ *                           corrupt keys are kept and restart the user key. */
+#define DLSM_SELECT_FLUSH 0
+#define DLSM_SELECT_COMPACTION 1
+
+/* ikeys: internal keys in iterator order (user key || Fixed64(seq<<8|type));
+ * its suffix_len is ignored.  keep_dev[i] (device, n bytes) = 1 iff the loop
+ * passes key i to Add.  Host outputs (any may be NULL): n_kept, kept_bytes (the
+ * kept keys' ExtractUserKey bytes), first_corrupt (index of the first key
+ * ParseInternalKey rejects, or UINT64_MAX).  FLUSH returns DLSM_E_CORRUPT when
+ * there is one.  Synchronous.
+ * The full filter of the kept keys equals the full filter of ALL the keys with
+ * suffix_len = 8: every dropped entry repeats the user key of the entry before
+ * it, whose hash AddKey's consecutive dedup drops anyway -- so a filter build
+ * never has to wait for this selection. */
+int dlsm_internal_keys_select_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, int policy,
+                                  uint64_t smallest_snapshot, uint8_t* keep_dev, uint64_t* n_kept,
+                                  uint64_t* kept_bytes, uint64_t* first_corrupt);
+
+/* Pack ExtractUserKey(key) of every key with keep_dev[i] != 0, in order.
+ * Fixed-length ikeys (key_len >= 8): user key j at user_keys_dev + j*(key_len-8),
+ * offsets_dev unused.  Variable-length ikeys: the bytes back to back and
+ * offsets_dev[0..n_kept] (device u64).  Size the outputs from
+ * dlsm_internal_keys_select_dev's n_kept / kept_bytes.  Asynchronous. */
+int dlsm_user_keys_gather_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, const uint8_t* keep_dev,
+                              uint8_t* user_keys_dev, uint64_t* offsets_dev);
 
 /* ---- full filter, probe ------------------------------------------------- */
 

@@ -84,7 +84,7 @@ class FullFilterBlockBuilder {
     job.keys.bytes = reinterpret_cast<const uint8_t*>(keys_.data());
     job.keys.offsets = offsets_.data();
     job.keys.key_len = 0;
-    job.keys.reserved = 0;
+    job.keys.suffix_len = 0;
     job.keys.n = offsets_.size() - 1;
     job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
     job.out_cap = local_mr_->length - static_cast<size_t>(result.data() - static_cast<char*>(local_mr_->addr));

@@ -55,6 +55,9 @@ def lib():
         L.orc_full_dedup_count.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64]
         L.orc_full_build.restype = C.c_int64
         L.orc_full_build.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, C.c_int, u8p, C.c_uint64]
+        L.orc_internal_keys_select.restype = C.c_int64
+        L.orc_internal_keys_select.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, C.c_int,
+                                               C.c_uint64, u8p, u64p]
         L.orc_full_reader_parse.argtypes = [u8p, C.c_uint64, C.POINTER(C.c_int),
                                             C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         L.orc_full_key_may_match.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t]
@@ -174,6 +177,22 @@ def full_build(keys: np.ndarray, n: int, stride: int = 20, offsets=None, bpk: in
 
 def full_dedup_count(keys, n, stride=20, offsets=None) -> int:
     return int(lib().orc_full_dedup_count(_ptr(keys), _ptr(offsets, u64p), stride, n))
+
+
+def internal_keys_select(keys: np.ndarray, n: int, policy: int, snapshot: int,
+                         stride: int = 28, offsets=None):
+    """Flush (policy 0) / compaction (1) selection over internal keys:
+    returns (keep u8[n], n_kept or -1 when a flush aborts, first_corrupt)."""
+    keep = np.zeros(max(n, 1), dtype=np.uint8)
+    bad = np.zeros(1, dtype=np.uint64)
+    r = lib().orc_internal_keys_select(_ptr(keys), _ptr(offsets, u64p), stride, n, policy, snapshot,
+                                       _ptr(keep), _ptr(bad, u64p))
+    return keep[:n], int(r), int(bad[0])
+
+
+def internal_key(user_key: bytes, seq: int, vtype: int = 1) -> bytes:
+    """user_key || Fixed64(seq << 8 | type) (db/dbformat.h:115-118, AppendInternalKey)."""
+    return user_key + ((seq << 8) | vtype).to_bytes(8, "little")
 
 
 def full_reader_parse(filt: bytes):

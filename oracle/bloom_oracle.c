@@ -531,3 +531,65 @@ uint32_t orc_crc32c_extend(uint32_t crc, const uint8_t* p, uint64_t n) {
   return ~c;
 }
 uint32_t orc_crc32c_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+
+/* ------------------------------------------------------------------------
+ * Internal-key selection: the loops that feed TableBuilder::Add, restated
+ * statement by statement (sequential state machine, as the reference runs it).
+ *   policy 0 = FlushJob::BuildTable          db/memtable_list.cc:855-886
+ *   policy 1 = DBImpl::DoCompactionWork      db/db_impl.cc:3500-3562
+ * ParseInternalKey db/dbformat.h:451-461.  keep[i] = 1 iff Add(key i) runs.
+ * Returns the number kept; *first_corrupt = index of the first unparsable key
+ * or UINT64_MAX.  For the flush the reference stops at that key (IOError,
+ * builder deleted): keep[] past it stays 0 and the return value is -1.
+ * ------------------------------------------------------------------------ */
+static int orc_parse_internal_key(const uint8_t* k, size_t n, uint64_t* seq) {
+  if (n < 8) return 0;
+  uint64_t num = 0;
+  for (int b = 0; b < 8; b++) num |= (uint64_t)k[n - 8 + b] << (8 * b); /* DecodeFixed64 */
+  *seq = num >> 8;
+  return (num & 0xff) <= 1; /* c <= kTypeValue */
+}
+
+int64_t orc_internal_keys_select(const uint8_t* bytes, const uint64_t* offsets, uint32_t stride,
+                                 uint64_t n, int policy, uint64_t smallest_snapshot,
+                                 uint8_t* keep, uint64_t* first_corrupt) {
+  const uint64_t kMaxSequenceNumber = ((uint64_t)1 << 56) - 1; /* db/dbformat.h */
+  const uint8_t* cur = NULL; /* current_user_key */
+  size_t cur_len = 0;
+  int has_current_user_key = 0;
+  uint64_t last_sequence_for_key = kMaxSequenceNumber;
+  int64_t kept = 0;
+  *first_corrupt = UINT64_MAX;
+  for (uint64_t i = 0; i < n; i++) keep[i] = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    size_t len;
+    const uint8_t* key = key_at(bytes, offsets, stride, i, &len);
+    uint64_t seq = 0;
+    int drop = 0;
+    if (!orc_parse_internal_key(key, len, &seq)) {
+      if (*first_corrupt == UINT64_MAX) *first_corrupt = i;
+      has_current_user_key = 0;
+      if (policy == 0) return -1; /* flush: "Corrupt key value detected", break */
+      last_sequence_for_key = kMaxSequenceNumber;
+    } else {
+      const size_t ulen = len - 8;
+      if (!has_current_user_key || ulen != cur_len || memcmp(key, cur, ulen) != 0) {
+        cur = key; /* current_user_key.assign(ikey.user_key) */
+        cur_len = ulen;
+        has_current_user_key = 1;
+        last_sequence_for_key = kMaxSequenceNumber;
+      } else if (policy == 0) {
+        drop = 1;
+      }
+      if (policy == 1) {
+        if (last_sequence_for_key <= smallest_snapshot) drop = 1; /* (A) */
+        last_sequence_for_key = seq;
+      }
+    }
+    if (!drop) {
+      keep[i] = 1;
+      kept++;
+    }
+  }
+  return kept;
+}
