@@ -27,7 +27,7 @@ __all__ = [
     "Keys", "Context", "FilterSet", "DlsmError", "device_available", "bloom_hash",
     "full_size", "legacy_size", "full_parse", "FullFilterBlockBuilder",
     "FullFilterBlockReader", "BloomFilterPolicy", "PATH_AUTO", "PATH_DIRECT", "PATH_SLICED",
-    "crc32c", "crc32c_mask",
+    "crc32c", "crc32c_mask", "Version", "VersionFile",
 ]
 
 PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
@@ -117,6 +117,61 @@ class Keys:
             offs[1:] = np.cumsum([len(k) for k in keys])
         data = np.frombuffer(b"".join(keys) + b"\0" * 16, dtype=np.uint8).copy()
         return Keys(data, len(keys), 0, offs)
+
+
+@dataclass
+class VersionFile:
+    """One SSTable of a version (RemoteMemTableMetaData's smallest / largest /
+    number + its full filter).  ``largest_trailer`` = seq << 8 | type of the
+    largest internal key; ``filter`` = bytes (host) or a device uint8 tensor,
+    or None for a table without a filter."""
+    level: int
+    number: int
+    smallest: bytes
+    largest: bytes
+    largest_trailer: int
+    filter: object = None
+
+
+class Version:
+    """A version's files and filters resident on one device (search order:
+    level-0 newest first, then one candidate per level 1..5)."""
+    NUM_LEVELS = 6
+
+    def __init__(self, ctx: "Context", files: Sequence[VersionFile], on_device: bool = False):
+        n = len(files)
+        arr = (_L.dlsm_version_file * max(n, 1))()
+        keep = []
+        for j, f in enumerate(files):
+            sm = np.frombuffer(bytes(f.smallest) + b"\0", dtype=np.uint8)
+            lg = np.frombuffer(bytes(f.largest) + b"\0", dtype=np.uint8)
+            keep += [sm, lg]
+            if f.filter is None:
+                fp, fl = None, 0
+            elif on_device:
+                fp, fl = _ptr(f.filter), int(f.filter.numel())
+            else:
+                fa = np.frombuffer(bytes(f.filter), dtype=np.uint8)
+                keep.append(fa)
+                fp, fl = fa.ctypes.data, fa.size
+            arr[j] = _L.dlsm_version_file(sm.ctypes.data, len(f.smallest), lg.ctypes.data,
+                                          len(f.largest), f.largest_trailer, f.number, f.level, 0,
+                                          fp, fl)
+        h = C.c_void_p()
+        check(lib().dlsm_version_create(ctx.h, arr, n, 1 if on_device else 0, C.byref(h)),
+              "version_create")
+        self.h = h
+        a, b = C.c_int(), C.c_int()
+        check(lib().dlsm_version_slots(h, C.byref(a), C.byref(b)), "version_slots")
+        self.n_l0, self.n_slots = a.value, b.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().dlsm_version_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
 
 
 class FilterSet:
@@ -290,6 +345,18 @@ class Context:
         ks = keys.c()
         check(lib().dlsm_user_keys_gather_dev(self.h, C.byref(ks), _ptr(keep), _ptr(out), _ptr(offsets)),
               "user_keys_gather_dev")
+
+    # -- MultiGet-style probe of a version -------------------------------------
+    def version(self, files: Sequence[VersionFile], on_device: bool = False) -> Version:
+        return Version(self, files, on_device)
+
+    def version_probe_dev(self, v: Version, keys: Keys, snapshot: int, slot_mask, level_file=None):
+        """slot_mask (device uint64[n]): bit s = search slot s is a file Version::Get
+        visits and whose filter passes the key; level_file (device int32/uint32
+        [n, 5], optional): per level the candidate file's index in the level."""
+        ks = keys.c()
+        check(lib().dlsm_version_probe_dev(self.h, v.h, C.byref(ks), snapshot, _ptr(slot_mask),
+                                           _ptr(level_file)), "version_probe_dev")
 
     # -- full filter probe --------------------------------------------------
     def filterset(self, filters, on_device: bool = False) -> FilterSet:

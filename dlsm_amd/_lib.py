@@ -34,6 +34,14 @@ class dlsm_build_job(C.Structure):
     _fields_ = [("keys", dlsm_keyset), ("out", C.c_void_p), ("out_cap", C.c_uint64)]
 
 
+class dlsm_version_file(C.Structure):
+    _fields_ = [("smallest_user_key", C.c_void_p), ("smallest_len", C.c_uint64),
+                ("largest_user_key", C.c_void_p), ("largest_len", C.c_uint64),
+                ("largest_trailer", C.c_uint64), ("number", C.c_uint64),
+                ("level", C.c_int32), ("reserved", C.c_int32),
+                ("filter", C.c_void_p), ("filter_len", C.c_uint64)]
+
+
 class DlsmError(RuntimeError):
     def __init__(self, status: int, what: str = ""):
         self.status = status
@@ -79,6 +87,11 @@ SIGNATURES = [
     ("dlsm_internal_keys_select_dev", C.c_int, [_VP, C.POINTER(dlsm_keyset), C.c_int, C.c_uint64,
                                                 _VP, _U64P, _U64P, _U64P]),
     ("dlsm_user_keys_gather_dev", C.c_int, [_VP, C.POINTER(dlsm_keyset), _VP, _VP, _VP]),
+    ("dlsm_version_create", C.c_int, [_VP, C.POINTER(dlsm_version_file), C.c_int, C.c_int,
+                                      C.POINTER(_VP)]),
+    ("dlsm_version_destroy", C.c_int, [_VP]),
+    ("dlsm_version_slots", C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    ("dlsm_version_probe_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), C.c_uint64, _VP, _VP]),
     ("dlsm_bloom_full_probe", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_legacy_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),

@@ -994,6 +994,147 @@ int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_ke
 }
 
 // ---------------------------------------------------------------------------
+// Version: files + filters for the MultiGet-style probe (§8f row 3)
+// ---------------------------------------------------------------------------
+static_assert(DLSM_NUM_LEVELS == kNumLevels, "config::kNumLevels");
+
+struct dlsm_version {
+  int device = 0;
+  VersionDev v{};
+  int n_files = 0;
+  uint8_t* mem = nullptr;  // one allocation: files | key blob | filters
+};
+
+int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_files,
+                        int filters_are_device, dlsm_version** out) {
+  if (!ctx || !out || n_files < 0 || (n_files > 0 && !files)) return DLSM_E_ARG;
+  *out = nullptr;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  // search order: level 0 newest first (NewestFirst, version_set.cc:268-270),
+  // then each level >= 1 in the caller's (key) order
+  std::vector<int> order;
+  int n_l0 = 0;
+  uint32_t begin[kNumLevels] = {}, count[kNumLevels] = {};
+  for (int f = 0; f < n_files; f++) {
+    const dlsm_version_file& F = files[f];
+    if (F.level < 0 || F.level >= kNumLevels) return DLSM_E_ARG;
+    if ((F.smallest_len && !F.smallest_user_key) || (F.largest_len && !F.largest_user_key)) return DLSM_E_ARG;
+    if (F.smallest_len > 0xffffffffull || F.largest_len > 0xffffffffull) return DLSM_E_ARG;
+    if (F.level == 0) n_l0++;
+  }
+  if (n_l0 > 64 - (kNumLevels - 1)) return DLSM_E_ARG;
+  for (int f = 0; f < n_files; f++)
+    if (files[f].level == 0) order.push_back(f);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return files[a].number > files[b].number; });
+  for (int lv = 1; lv < kNumLevels; lv++) {
+    begin[lv] = static_cast<uint32_t>(order.size());
+    for (int f = 0; f < n_files; f++)
+      if (files[f].level == lv) order.push_back(f);
+    count[lv] = static_cast<uint32_t>(order.size()) - begin[lv];
+  }
+  // layout: VFileDev[n] | key blob | filters (each 256-B aligned)
+  std::vector<VFileDev> h(n_files);
+  std::vector<uint8_t> keys;
+  std::vector<uint64_t> foff(n_files, 0);
+  const uint64_t files_bytes = (sizeof(VFileDev) * n_files + 255) & ~uint64_t(255);
+  for (int j = 0; j < n_files; j++) {
+    const dlsm_version_file& F = files[order[j]];
+    VFileDev& d = h[j];
+    d.smallest_off = keys.size();
+    d.smallest_len = static_cast<uint32_t>(F.smallest_len);
+    keys.insert(keys.end(), F.smallest_user_key, F.smallest_user_key + F.smallest_len);
+    d.largest_off = keys.size();
+    d.largest_len = static_cast<uint32_t>(F.largest_len);
+    keys.insert(keys.end(), F.largest_user_key, F.largest_user_key + F.largest_len);
+    d.largest_trailer = F.largest_trailer;
+    d.f = FilterDev{};
+  }
+  const uint64_t keys_bytes = (keys.size() + 255) & ~uint64_t(255);
+  uint64_t total = files_bytes + keys_bytes;
+  for (int j = 0; j < n_files; j++) {
+    const dlsm_version_file& F = files[order[j]];
+    if (!F.filter) continue;
+    if (F.filter_len < 5) return DLSM_E_CORRUPT;
+    uint8_t tail[5];
+    if (filters_are_device) {
+      DLSM_TRY(hipMemcpyAsync(tail, F.filter + F.filter_len - 5, 5, hipMemcpyDeviceToHost, s));
+      DLSM_TRY(hipStreamSynchronize(s));
+    } else {
+      memcpy(tail, F.filter + F.filter_len - 5, 5);
+    }
+    int k, lg;
+    uint32_t L;
+    DLSM_CHECK(parse_tail(tail, F.filter_len, &k, &L, &lg));
+    h[j].f.L = L;
+    h[j].f.magic = fastmod_magic(L);
+    h[j].f.k = k;
+    h[j].f.lg = lg;
+    foff[j] = total;
+    total += (F.filter_len + 255) & ~uint64_t(255);
+  }
+  dlsm_version* ver = new (std::nothrow) dlsm_version();
+  if (!ver) return DLSM_E_NOMEM;
+  ver->device = ctx->device;
+  ver->n_files = n_files;
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&ver->mem), std::max<uint64_t>(total, 256));
+  for (int j = 0; j < n_files && e == hipSuccess; j++) {
+    const dlsm_version_file& F = files[order[j]];
+    if (!F.filter) continue;
+    h[j].f.data = ver->mem + foff[j];
+    e = hipMemcpyAsync(ver->mem + foff[j], F.filter, F.filter_len,
+                       filters_are_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s);
+  }
+  if (e == hipSuccess && n_files)
+    e = hipMemcpyAsync(ver->mem, h.data(), sizeof(VFileDev) * n_files, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && !keys.empty())
+    e = hipMemcpyAsync(ver->mem + files_bytes, keys.data(), keys.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // pageable sources: finish before returning
+  if (e != hipSuccess) {
+    dlsm_version_destroy(ver);
+    return from_hip(e);
+  }
+  ver->v.files = reinterpret_cast<const VFileDev*>(ver->mem);
+  ver->v.keyblob = ver->mem + files_bytes;
+  ver->v.n_l0 = static_cast<uint32_t>(n_l0);
+  for (int lv = 0; lv < kNumLevels; lv++) {
+    ver->v.lvl_begin[lv] = begin[lv];
+    ver->v.lvl_count[lv] = count[lv];
+  }
+  *out = ver;
+  return DLSM_OK;
+}
+
+int dlsm_version_destroy(dlsm_version* v) {
+  if (!v) return DLSM_OK;
+  DeviceGuard g(v->device);
+  if (v->mem) (void)hipFree(v->mem);
+  delete v;
+  return DLSM_OK;
+}
+
+int dlsm_version_slots(const dlsm_version* v, int* n_l0, int* n_slots) {
+  if (!v) return DLSM_E_ARG;
+  if (n_l0) *n_l0 = static_cast<int>(v->v.n_l0);
+  if (n_slots) *n_slots = static_cast<int>(v->v.n_l0) + kNumLevels - 1;
+  return DLSM_OK;
+}
+
+int dlsm_version_probe_dev(dlsm_ctx* ctx, const dlsm_version* v, const dlsm_keyset* keys,
+                           uint64_t snapshot, uint64_t* slot_mask_dev, uint32_t* level_file_dev) {
+  if (!ctx || !v || !keys) return DLSM_E_ARG;
+  if (v->device != ctx->device) return DLSM_E_ARG;
+  if (snapshot > ((uint64_t(1) << 56) - 1)) return DLSM_E_ARG;  // kMaxSequenceNumber
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!slot_mask_dev) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  DLSM_TRY(launch_version_probe(v->v, to_desc(*keys), snapshot, slot_mask_dev, level_file_dev, ctx->stream));
+  return DLSM_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Legacy FilterPolicy format (util/bloom.cc)
 // ---------------------------------------------------------------------------
 int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,

@@ -43,6 +43,25 @@ struct FilterDev {
   int32_t k, lg;
 };
 
+// One SSTable of a version (dlsm_version_file) as the version probe sees it.
+struct VFileDev {
+  uint64_t smallest_off, largest_off;  // user keys inside the version's key blob
+  uint32_t smallest_len, largest_len;
+  uint64_t largest_trailer;            // seq << 8 | type of the largest internal key
+  FilterDev f;                         // f.data == nullptr: the table has no filter
+};
+
+constexpr int kNumLevels = 6;  // config::kNumLevels (db/dbformat.h:26)
+
+// Files in search order: level-0 newest first, then levels 1.. in key order.
+struct VersionDev {
+  const VFileDev* files;
+  const uint8_t* keyblob;
+  uint32_t n_l0;
+  uint32_t lvl_begin[kNumLevels];
+  uint32_t lvl_count[kNumLevels];
+};
+
 // Legacy-format build job.
 struct LegacyJobDev {
   KeyDesc keys;
@@ -92,6 +111,8 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                   uint8_t* mask, int lgC, hipStream_t s);
 
+hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
+                                uint64_t* slot_mask, uint32_t* level_file, hipStream_t s);
 hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s, int n_jobs,
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,

@@ -975,6 +975,77 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
 }
 
 // ---------------------------------------------------------------------------
+// MultiGet-style probe of a version: per lookup key,
+// the files Version::ForEachOverlapping (db/version_set.cc:273-321) visits --
+// level-0 files whose user-key range holds the key, newest first, then per
+// level the file FindFile (:95-118) picks -- whose filter passes the key
+// (Table::InternalGet, table/table.cc:350-358).  One thread per key; the key
+// is hashed once (the reference re-hashes per file: same value).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int bytewise_cmp(const uint8_t* a, uint64_t an, const uint8_t* b, uint64_t bn) {
+  // BytewiseComparator: memcmp over the shorter length, then the length
+  const uint64_t n = an < bn ? an : bn;
+  for (uint64_t j = 0; j < n; j++) {
+    const int d = static_cast<int>(a[j]) - static_cast<int>(b[j]);
+    if (d) return d;
+  }
+  return an < bn ? -1 : (an > bn ? 1 : 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
+                                                               uint64_t* __restrict__ slot_mask,
+                                                               uint32_t* __restrict__ level_file) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x;
+  if (i >= kd.n) return;
+  uint64_t s, l;
+  if (kd.offsets) {
+    s = kd.offsets[i];
+    l = kd.offsets[i + 1] - s;
+  } else {
+    s = i * kd.key_len;
+    l = kd.key_len;
+  }
+  l = l > kd.suffix ? l - kd.suffix : 0;  // ExtractUserKey
+  const uint8_t* uk = kd.bytes + s;
+  const uint32_t h = key_hash<MODE>(kd, i);
+  // LookupKey(user_key, snapshot): trailer PackSequenceAndType(snapshot, kValueTypeForSeek)
+  const uint64_t tnum = (snapshot << 8) | 1u;
+  uint64_t m = 0;
+  for (uint32_t f = 0; f < v.n_l0; f++) {  // level 0: newest first
+    const VFileDev& F = v.files[f];
+    if (bytewise_cmp(uk, l, v.keyblob + F.smallest_off, F.smallest_len) >= 0 &&
+        bytewise_cmp(uk, l, v.keyblob + F.largest_off, F.largest_len) <= 0 &&
+        (F.f.data == nullptr || full_may_match(h, F.f)))
+      m |= 1ull << f;
+  }
+  for (int lv = 1; lv < kNumLevels; lv++) {
+    const uint32_t nf = v.lvl_count[lv];
+    uint32_t pick = 0xffffffffu;
+    if (nf) {
+      const VFileDev* fl = v.files + v.lvl_begin[lv];
+      // FindFile: earliest file whose largest internal key >= the lookup key
+      // (right starts at nf-1, so the last file is picked when none is >=)
+      uint32_t left = 0, right = nf - 1;
+      while (left < right) {
+        const uint32_t mid = (left + right) / 2;
+        int r = bytewise_cmp(v.keyblob + fl[mid].largest_off, fl[mid].largest_len, uk, l);
+        if (r == 0) r = fl[mid].largest_trailer > tnum ? -1 : (fl[mid].largest_trailer < tnum ? 1 : 0);
+        if (r < 0) left = mid + 1;
+        else right = mid;
+      }
+      const VFileDev& F = fl[right];
+      if (bytewise_cmp(uk, l, v.keyblob + F.smallest_off, F.smallest_len) >= 0) {
+        pick = right;
+        if (F.f.data == nullptr || full_may_match(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
+      }
+    }
+    if (level_file) level_file[i * (kNumLevels - 1) + (lv - 1)] = pick;
+  }
+  slot_mask[i] = m;
+}
+
+// ---------------------------------------------------------------------------
 // Legacy FilterPolicy format (util/bloom.cc): global double hashing.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t legacy_bitpos(uint32_t h, uint64_t bits, uint32_t magic) {
@@ -1216,6 +1287,18 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
     case 14: probe_unpermute_kernel<16384><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
+                                uint64_t* slot_mask, uint32_t* level_file, hipStream_t s) {
+  if (keys.n == 0) return hipSuccess;
+  const unsigned g = static_cast<unsigned>((keys.n + kBlock - 1) / kBlock);
+  if (keys.offsets == nullptr && keys.key_len == 20 && keys.suffix == 0 &&
+      (reinterpret_cast<uintptr_t>(keys.bytes) & 3u) == 0)
+    version_probe_kernel<KM_K20><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+  else
+    version_probe_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
   return hipGetLastError();
 }
 

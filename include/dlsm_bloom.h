@@ -233,6 +233,56 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
 int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
                           uint8_t* mask);
 
+/* ---- MultiGet-style probe of a version's files ---- */
+
+/* One SSTable of a version: its key range and its full filter.  Mirrors
+ * RemoteMemTableMetaData's smallest / largest InternalKeys and number
+ * (db/version_edit.h) and the table's FullFilterBlockReader. */
+typedef struct {
+  const uint8_t* smallest_user_key; /* host memory */
+  uint64_t smallest_len;
+  const uint8_t* largest_user_key; /* host memory */
+  uint64_t largest_len;
+  uint64_t largest_trailer; /* DecodeFixed64 of largest's last 8 bytes: seq << 8 | type */
+  uint64_t number;          /* file number: level-0 files are searched largest first */
+  int32_t level;            /* 0 .. DLSM_NUM_LEVELS-1 */
+  int32_t reserved;
+  const uint8_t* filter; /* full filter bytes, or NULL: a table without a filter */
+  uint64_t filter_len;
+} dlsm_version_file;
+
+#define DLSM_NUM_LEVELS 6 /* config::kNumLevels, db/dbformat.h:26 */
+
+typedef struct dlsm_version dlsm_version; /* the files and filters, resident on a device */
+
+/* files: every SSTable of the version; within each level >= 1 in key order
+ * (Version::levels_, non-overlapping), level-0 files in any order.  At most
+ * 64 - (DLSM_NUM_LEVELS - 1) level-0 files.  filters_are_device: the filter
+ * pointers are device pointers on ctx's device (key bounds are host memory
+ * either way).  Filters are parsed like FullFilterBlockReader (DLSM_E_CORRUPT
+ * where it exit(1)s or cannot probe). */
+int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_files,
+                        int filters_are_device, dlsm_version** out);
+int dlsm_version_destroy(dlsm_version* v);
+/* Search slots: 0 .. n_l0-1 = level-0 files newest first (largest number
+ * first); n_l0 + level - 1 = the one candidate file of level 1..5. */
+int dlsm_version_slots(const dlsm_version* v, int* n_l0, int* n_slots);
+
+/* For every lookup key (user keys; suffix_len 8 for internal keys), the files
+ * Version::Get would visit -- Version::ForEachOverlapping (db/version_set.cc:
+ * 273-321): level-0 files whose [smallest, largest] user-key range holds the
+ * key, newest first, then per level the file FindFile (:95-118) picks for
+ * LookupKey(key, snapshot) (db/dbformat.cc:111-128) unless the key sorts
+ * before its smallest key -- whose filter passes the key (Table::InternalGet,
+ * table/table.cc:350-358: FullFilterBlockReader::KeyMayMatch, or always when
+ * the table has no filter).  slot_mask_dev[i] (device u64): bit s set for such
+ * a file in search slot s; a Get reads the set slots in increasing order and
+ * stops at the first that holds the key.  level_file_dev (device u32, n x
+ * (DLSM_NUM_LEVELS-1), or NULL): per level the index inside that level of the
+ * candidate file, UINT32_MAX when the level has none.  Asynchronous. */
+int dlsm_version_probe_dev(dlsm_ctx* ctx, const dlsm_version* v, const dlsm_keyset* keys,
+                           uint64_t snapshot, uint64_t* slot_mask_dev, uint32_t* level_file_dev);
+
 /* ---- legacy FilterPolicy format (util/bloom.cc) ------------------------- */
 
 /* CreateFilter(keys, n, dst) per job: writes bytes+1 bytes at out.

@@ -58,6 +58,8 @@ def lib():
         L.orc_internal_keys_select.restype = C.c_int64
         L.orc_internal_keys_select.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, C.c_int,
                                                C.c_uint64, u8p, u64p]
+        L.orc_version_probe.argtypes = [C.c_void_p, C.c_int, u8p, u64p, C.c_uint32, C.c_uint32,
+                                        C.c_uint64, C.c_uint64, u64p, C.POINTER(C.c_uint32)]
         L.orc_full_reader_parse.argtypes = [u8p, C.c_uint64, C.POINTER(C.c_int),
                                             C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         L.orc_full_key_may_match.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t]
@@ -193,6 +195,40 @@ def internal_keys_select(keys: np.ndarray, n: int, policy: int, snapshot: int,
 def internal_key(user_key: bytes, seq: int, vtype: int = 1) -> bytes:
     """user_key || Fixed64(seq << 8 | type) (db/dbformat.h:115-118, AppendInternalKey)."""
     return user_key + ((seq << 8) | vtype).to_bytes(8, "little")
+
+
+class _VFile(C.Structure):  # same layout as dlsm_version_file
+    _fields_ = [("smallest", C.c_void_p), ("smallest_len", C.c_uint64),
+                ("largest", C.c_void_p), ("largest_len", C.c_uint64),
+                ("largest_trailer", C.c_uint64), ("number", C.c_uint64),
+                ("level", C.c_int32), ("reserved", C.c_int32),
+                ("filter", C.c_void_p), ("filter_len", C.c_uint64)]
+
+
+def version_probe(files, keys: np.ndarray, n: int, snapshot: int, stride: int = 20,
+                  offsets=None, suffix: int = 0):
+    """ForEachOverlapping + FindFile + the filter check, restated
+    (orc_version_probe).  files: objects with level, number, smallest, largest,
+    largest_trailer, filter (bytes or None).  Returns (mask u64[n], level_file u32[n, 5])."""
+    arr = (_VFile * max(len(files), 1))()
+    keep = []
+    for j, f in enumerate(files):
+        sm = np.frombuffer(bytes(f.smallest) + b"\0", dtype=np.uint8)
+        lg = np.frombuffer(bytes(f.largest) + b"\0", dtype=np.uint8)
+        keep += [sm, lg]
+        fp, fl = None, 0
+        if f.filter is not None:
+            fa = np.frombuffer(bytes(f.filter), dtype=np.uint8)
+            keep.append(fa)
+            fp, fl = fa.ctypes.data, fa.size
+        arr[j] = _VFile(sm.ctypes.data, len(f.smallest), lg.ctypes.data, len(f.largest),
+                        f.largest_trailer, f.number, f.level, 0, fp, fl)
+    mask = np.zeros(max(n, 1), dtype=np.uint64)
+    lf = np.zeros((max(n, 1), 5), dtype=np.uint32)
+    st = lib().orc_version_probe(arr, len(files), _ptr(keys), _ptr(offsets, u64p), stride, suffix, n,
+                                 snapshot, _ptr(mask, u64p), lf.ctypes.data_as(C.POINTER(C.c_uint32)))
+    assert st == 0, st
+    return mask[:n], lf[:n]
 
 
 def full_reader_parse(filt: bytes):

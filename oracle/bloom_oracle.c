@@ -593,3 +593,109 @@ int64_t orc_internal_keys_select(const uint8_t* bytes, const uint64_t* offsets, 
   }
   return kept;
 }
+
+/* ------------------------------------------------------------------------
+ * Version::ForEachOverlapping + FindFile + Table::InternalGet's filter check,
+ * restated (db/version_set.cc:95-118, 268-321; table/table.cc:350-358;
+ * db/dbformat.cc:41-57 InternalKeyComparator, :111-128 LookupKey).
+ * The layout of orc_version_file matches dlsm_version_file.
+ * For each key: out_mask bit s for every file Match() would be called on whose
+ * filter passes the key (slot s: level-0 rank newest first, then
+ * n_l0 + level - 1); out_level_file[i*5 + level-1] = FindFile's pick inside
+ * the level or UINT32_MAX.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  const uint8_t* smallest;
+  uint64_t smallest_len;
+  const uint8_t* largest;
+  uint64_t largest_len;
+  uint64_t largest_trailer;
+  uint64_t number;
+  int32_t level;
+  int32_t reserved;
+  const uint8_t* filter;
+  uint64_t filter_len;
+} orc_version_file;
+
+static int orc_bytewise(const uint8_t* a, size_t an, const uint8_t* b, size_t bn) { /* util/comparator.cc */
+  size_t n = an < bn ? an : bn;
+  int r = n ? memcmp(a, b, n) : 0;
+  if (r == 0) r = an < bn ? -1 : (an > bn ? 1 : 0);
+  return r;
+}
+
+/* InternalKeyComparator::Compare on (user key, trailer) pairs */
+static int orc_icmp(const uint8_t* a, size_t an, uint64_t anum, const uint8_t* b, size_t bn, uint64_t bnum) {
+  int r = orc_bytewise(a, an, b, bn);
+  if (r == 0) {
+    if (anum > bnum) r = -1;
+    else if (anum < bnum) r = +1;
+  }
+  return r;
+}
+
+int orc_version_probe(const orc_version_file* files, int n_files, const uint8_t* bytes,
+                      const uint64_t* offsets, uint32_t stride, uint32_t suffix, uint64_t n,
+                      uint64_t snapshot, uint64_t* out_mask, uint32_t* out_level_file) {
+  enum { kNumLevels = 6 };
+  int l0[64], n_l0 = 0;
+  int lvl[kNumLevels][4096];
+  int nlvl[kNumLevels] = {0};
+  for (int f = 0; f < n_files; f++) {
+    if (files[f].level == 0) {
+      if (n_l0 == 64) return ORC_E_ARG;
+      l0[n_l0++] = f;
+    } else {
+      if (nlvl[files[f].level] == 4096) return ORC_E_ARG;
+      lvl[files[f].level][nlvl[files[f].level]++] = f;
+    }
+  }
+  /* level-0 slot = rank by number, largest first (NewestFirst) */
+  for (int a = 1; a < n_l0; a++)
+    for (int b = a; b > 0 && files[l0[b]].number > files[l0[b - 1]].number; b--) {
+      int t = l0[b]; l0[b] = l0[b - 1]; l0[b - 1] = t;
+    }
+  const uint64_t tnum = (snapshot << 8) | 1; /* PackSequenceAndType(s, kValueTypeForSeek) */
+  for (uint64_t i = 0; i < n; i++) {
+    size_t len;
+    const uint8_t* key = key_at(bytes, offsets, stride, i, &len);
+    size_t ulen = len > suffix ? len - suffix : 0;
+    uint64_t m = 0;
+    for (int j = 0; j < n_l0; j++) { /* tmp: overlapping level-0 files, newest first */
+      const orc_version_file* F = &files[l0[j]];
+      if (orc_bytewise(key, ulen, F->smallest, F->smallest_len) >= 0 &&
+          orc_bytewise(key, ulen, F->largest, F->largest_len) <= 0) {
+        /* Match -> TableCache::Get -> Table::InternalGet: filter check */
+        if (!F->filter || orc_full_key_may_match(F->filter, F->filter_len, key, ulen)) m |= 1ull << j;
+      }
+    }
+    for (int level = 1; level < kNumLevels; level++) {
+      uint32_t pick = UINT32_MAX;
+      int num_files = nlvl[level];
+      if (num_files != 0) {
+        /* FindFile: left = 0, right = files.size()-1 */
+        uint32_t left = 0, right = (uint32_t)num_files - 1;
+        while (left < right) {
+          uint32_t mid = (left + right) / 2;
+          const orc_version_file* F = &files[lvl[level][mid]];
+          if (orc_icmp(F->largest, F->largest_len, F->largest_trailer, key, ulen, tnum) < 0) left = mid + 1;
+          else right = mid;
+        }
+        uint32_t index = right;
+        if (index < (uint32_t)num_files) {
+          const orc_version_file* F = &files[lvl[level][index]];
+          if (orc_bytewise(key, ulen, F->smallest, F->smallest_len) < 0) {
+            /* All of "f" is past any data for user_key */
+          } else {
+            pick = index;
+            if (!F->filter || orc_full_key_may_match(F->filter, F->filter_len, key, ulen))
+              m |= 1ull << (n_l0 + level - 1);
+          }
+        }
+      }
+      if (out_level_file) out_level_file[i * (kNumLevels - 1) + (level - 1)] = pick;
+    }
+    out_mask[i] = m;
+  }
+  return 0;
+}

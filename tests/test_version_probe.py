@@ -1,0 +1,158 @@
+"""MultiGet-style probe of a version's files.
+
+For each lookup key the GPU returns the files Version::Get would visit --
+Version::ForEachOverlapping (db/version_set.cc:273-321: level-0 files holding
+the key newest first, then per level the file FindFile picks, :95-118) --
+whose filter passes the key (Table::InternalGet, table/table.cc:350-358).
+The oracle (``orc_version_probe``) restates those lines; the cases below are
+hand-derived from them, including the reference's FindFile quirk (right
+starts at files.size()-1, so a key past a level's last file still visits that
+file when it is >= its smallest key).  Parity unpinned by reference outputs
+(Version needs the RDMA Env to run).
+"""
+import numpy as np
+import pytest
+
+import oracle
+from dlsm_amd import VersionFile
+
+K = lambda v: oracle.keys_from_values(np.array([v], dtype=np.uint64)).tobytes()  # noqa: E731
+
+
+def build_filter(values):
+    keys = oracle.keys_from_values(np.asarray(values, dtype=np.uint64))
+    return oracle.full_build(keys, len(values))
+
+
+def make_version(seed=0, with_nofilter=True):
+    """L0: 4 overlapping files; L1: 8 range-partitioned files; L2: 16; L3 empty;
+    L4: 2; L5: 1 file (without a filter when with_nofilter)."""
+    rng = np.random.default_rng(seed)
+    files = []
+    span = 1_000_000
+    for j in range(4):  # level 0: overlapping ranges, numbers out of order
+        a = int(rng.integers(0, span // 2))
+        b = a + int(rng.integers(span // 10, span // 2))
+        vals = np.arange(a, b, 7 + j)
+        files.append(VersionFile(0, int(rng.integers(100, 200)) * 10 + j, K(vals[0]), K(vals[-1]),
+                                 (int(rng.integers(1, 1 << 40)) << 8) | 1, build_filter(vals)))
+    for level, nf, step in ((1, 8, 3), (2, 16, 5), (4, 2, 11)):
+        edges = np.linspace(0, span, nf + 1).astype(np.int64)
+        for q in range(nf):
+            vals = np.arange(edges[q] + q % 3, edges[q + 1] - 1, step)
+            files.append(VersionFile(level, 1000 + level * 100 + q, K(vals[0]), K(vals[-1]),
+                                     (int(rng.integers(1, 1 << 40)) << 8) | 1, build_filter(vals)))
+    vals = np.arange(100, span // 2, 13)
+    files.append(VersionFile(5, 7, K(vals[0]), K(vals[-1]), (5 << 8) | 1,
+                             None if with_nofilter else build_filter(vals)))
+    return files
+
+
+def lookups(n, seed=1):
+    rng = np.random.default_rng(seed)
+    v = np.concatenate([rng.integers(0, 1_300_000, n - 4), [0, 999_999, 1_000_000, 2_000_000]])
+    return oracle.keys_from_values(v.astype(np.uint64))
+
+
+def test_oracle_hand_cases():
+    """Level 1 has files [10..20] and [30..40]; level 0 files [15..35] (#9) and
+    [0..50] (#12).  Key 25: both L0 files (newest first: #12, #9), level 1
+    picks file 1 ([30..40], largest >= 25) and skips it (25 < 30).  Key 45:
+    L0 #12 only; level 1 FindFile returns the last file (the quirk) and it is
+    visited (45 >= 30).  Key 5: L0 #12 only; level 1 picks file 0 and skips it
+    (5 < 10).  No filters: every candidate passes."""
+    t = (1 << 8) | 1
+    files = [VersionFile(1, 1, K(10), K(20), t), VersionFile(1, 2, K(30), K(40), t),
+             VersionFile(0, 9, K(15), K(35), t), VersionFile(0, 12, K(0), K(50), t)]
+    keys = np.frombuffer(K(25) + K(45) + K(5), dtype=np.uint8).copy()
+    mask, lf = oracle.version_probe(files, keys, 3, snapshot=100)
+    # slots: 0 = L0 #12, 1 = L0 #9, 2 = level 1, 3.. = levels 2..5
+    assert mask.tolist() == [0b011, 0b101, 0b001]
+    assert lf[:, 0].tolist() == [0xFFFFFFFF, 1, 0xFFFFFFFF]
+
+
+def test_oracle_findfile_snapshot_tiebreak():
+    """Key == a file's largest user key: FindFile compares internal keys; with
+    the lookup snapshot below the file's largest sequence the file's largest
+    sorts before the lookup key, so FindFile moves on to the next file."""
+    files = [VersionFile(1, 1, K(10), K(20), (50 << 8) | 1), VersionFile(1, 2, K(30), K(40), (9 << 8) | 1)]
+    keys = np.frombuffer(K(20), dtype=np.uint8).copy()
+    _, lf = oracle.version_probe(files, keys, 1, snapshot=60)
+    assert lf[0, 0] == 0
+    _, lf = oracle.version_probe(files, keys, 1, snapshot=40)
+    assert lf[0, 0] == 0xFFFFFFFF  # picks file 1 ([30..40]) and 20 < 30 skips it
+
+
+def test_oracle_filter_gates_candidates():
+    files = make_version(3, with_nofilter=False)
+    q = lookups(5000, 4)
+    mask, lf = oracle.version_probe(files, q, 5000, snapshot=1 << 45)
+    nofilt = [VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer, None) for f in files]
+    cand, lf2 = oracle.version_probe(nofilt, q, 5000, snapshot=1 << 45)
+    assert np.array_equal(lf, lf2)
+    assert np.all((mask & ~cand) == 0)       # the filter only removes candidates
+    assert (mask != cand).any() and mask.any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("snapshot", [1 << 45, 1 << 20])
+@pytest.mark.parametrize("on_device", [False, True])
+def test_gpu_version_probe(gpu, snapshot, on_device):
+    import torch
+
+    import dlsm_amd
+
+    files = make_version(0)
+    if on_device:
+        files = [VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer,
+                             None if f.filter is None else torch.frombuffer(bytearray(f.filter), dtype=torch.uint8).cuda())
+                 for f in files]
+    n = 200_003
+    q = lookups(n, 9)
+    want, want_lf = oracle.version_probe(make_version(0), q, n, snapshot)
+    v = gpu.version(files, on_device=on_device)
+    assert v.n_l0 == 4 and v.n_slots == 9
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snapshot, mask, lf)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_version_probe_internal_var_keys(gpu):
+    """Variable-length internal keys (suffix_len 8) against the same version."""
+    import torch
+
+    import dlsm_amd
+
+    files = make_version(2)
+    n = 30_000
+    q = lookups(n, 5)
+    ikeys = [q[20 * i: 20 * i + 20].tobytes() + ((77 << 8) | 1).to_bytes(8, "little") for i in range(n)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(k) for k in ikeys])
+    data = np.frombuffer(b"".join(ikeys) + b"\0" * 16, dtype=np.uint8).copy()
+    want, _ = oracle.version_probe(files, data, n, 1 << 30, offsets=offs, suffix=8)
+    v = gpu.version(files)
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    ks = dlsm_amd.Keys(torch.from_numpy(data).cuda(), n, 0, torch.from_numpy(offs).cuda(), suffix_len=8)
+    gpu.version_probe_dev(v, ks, 1 << 30, mask)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+    v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_version_rejects_bad_input(gpu):
+    import dlsm_amd
+
+    t = (1 << 8) | 1
+    with pytest.raises(dlsm_amd.DlsmError):  # too many level-0 files for 64 slots
+        gpu.version([VersionFile(0, j, K(0), K(9), t) for j in range(60)])
+    with pytest.raises(dlsm_amd.DlsmError):  # corrupt filter
+        gpu.version([VersionFile(1, 1, K(0), K(9), t, b"\x01\x02")])
+    with pytest.raises(dlsm_amd.DlsmError):  # level out of range
+        gpu.version([VersionFile(6, 1, K(0), K(9), t)])
