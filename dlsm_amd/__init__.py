@@ -346,6 +346,35 @@ class Context:
         check(lib().dlsm_user_keys_gather_dev(self.h, C.byref(ks), _ptr(keep), _ptr(out), _ptr(offsets)),
               "user_keys_gather_dev")
 
+    # -- legacy block-based filter block (table/filter_block.cc) -------------
+    def filter_block_build_dev(self, keys: Keys, block_key_end, block_end_offset,
+                               bits_per_key: int = 10, out=None):
+        """FilterBlockBuilder over a table's keys (data block b ends at key
+        block_key_end[b], then StartBlock(block_end_offset[b])).  Returns the
+        block as a device uint8 tensor (or fills `out` and returns its length)."""
+        import torch
+
+        ke = np.ascontiguousarray(block_key_end, dtype=np.uint64)
+        eo = np.ascontiguousarray(block_end_offset, dtype=np.uint64)
+        nb = C.c_uint64()
+        check(lib().dlsm_filter_block_size(_ptr(ke), _ptr(eo), len(ke), keys.n,
+                                           bits_per_key, C.byref(nb)), "filter_block_size")
+        ret = out is None
+        if out is None:
+            out = torch.empty(nb.value, dtype=torch.uint8, device=f"cuda:{self.device}")
+        ln = C.c_uint64()
+        ks = keys.c()
+        check(lib().dlsm_filter_block_build_dev(self.h, C.byref(ks), _ptr(ke), _ptr(eo),
+                                                len(ke), bits_per_key, _ptr(out), int(out.numel()),
+                                                C.byref(ln)), "filter_block_build_dev")
+        return out[: ln.value] if ret else ln.value
+
+    def filter_block_probe_dev(self, block, keys: Keys, block_offsets, out):
+        """FilterBlockReader::KeyMayMatch(block_offsets[i], key i) -> out[i] (device)."""
+        ks = keys.c()
+        check(lib().dlsm_filter_block_probe_dev(self.h, _ptr(block), int(block.numel()), C.byref(ks),
+                                                _ptr(block_offsets), _ptr(out)), "filter_block_probe_dev")
+
     # -- MultiGet-style probe of a version -------------------------------------
     def version(self, files: Sequence[VersionFile], on_device: bool = False) -> Version:
         return Version(self, files, on_device)

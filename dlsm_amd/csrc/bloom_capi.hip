@@ -994,6 +994,112 @@ int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_ke
 }
 
 // ---------------------------------------------------------------------------
+// Legacy block-based filter block (table/filter_block.cc), §8f row 4
+// ---------------------------------------------------------------------------
+namespace {
+constexpr uint64_t kFilterBaseLg = 11;  // filter_block.cc:15-16: a filter every 2 KiB
+
+// FilterBlockBuilder's filter groups for the StartBlock / AddKey sequence of a
+// TableBuilder: keys of data block b, then StartBlock(block_end_offset[b])
+// (TableBuilder::Flush); GenerateFilter takes every pending key (first loop
+// turn) or none (later turns); Finish generates one more if keys are pending.
+struct FilterGroups {
+  std::vector<uint64_t> begin, end;  // key range per filter (empty allowed)
+  std::vector<uint32_t> off;         // filter_offsets_
+  uint64_t array_offset = 0;
+  uint64_t total = 0;  // block length
+};
+
+int filter_groups(const uint64_t* block_key_end, const uint64_t* block_end_offset, int n_blocks,
+                  uint64_t n_keys, int bits_per_key, FilterGroups& G) {
+  if (n_blocks < 0 || (n_blocks > 0 && (!block_key_end || !block_end_offset))) return DLSM_E_ARG;
+  uint64_t pending = 0, prev_end = 0, result = 0;
+  auto generate = [&](uint64_t upto) {
+    G.off.push_back(static_cast<uint32_t>(result));
+    G.begin.push_back(pending);
+    G.end.push_back(upto);
+    if (upto > pending) result += legacy_bits(upto - pending, bits_per_key) / 8 + 1;  // CreateFilter
+    pending = upto;
+  };
+  for (int b = 0; b < n_blocks; b++) {
+    const uint64_t ke = block_key_end[b];
+    if (ke < prev_end || ke > n_keys) return DLSM_E_ARG;
+    prev_end = ke;
+    const uint64_t index = block_end_offset[b] / (uint64_t(1) << kFilterBaseLg);
+    if (index < G.off.size()) return DLSM_E_ARG;  // assert(filter_index >= filter_offsets_.size())
+    while (index > G.off.size()) generate(ke);     // later turns: no pending keys -> empty
+  }
+  if (n_keys > pending) generate(n_keys);  // Finish: start_ not empty
+  G.array_offset = result;
+  G.total = result + 4 * G.off.size() + 4 + 1;
+  if (G.array_offset > 0xffffffffull) return DLSM_E_ARG;  // Fixed32 offsets
+  return DLSM_OK;
+}
+}  // namespace
+
+int dlsm_filter_block_size(const uint64_t* block_key_end, const uint64_t* block_end_offset,
+                           int n_blocks, uint64_t n_keys, int bits_per_key, uint64_t* nbytes) {
+  if (!nbytes) return DLSM_E_ARG;
+  FilterGroups G;
+  DLSM_CHECK(filter_groups(block_key_end, block_end_offset, n_blocks, n_keys, bits_per_key, G));
+  *nbytes = G.total;
+  return DLSM_OK;
+}
+
+int dlsm_filter_block_build_dev(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64_t* block_key_end,
+                                const uint64_t* block_end_offset, int n_blocks, int bits_per_key,
+                                uint8_t* out_dev, uint64_t out_cap, uint64_t* out_len) {
+  if (!ctx || !keys || !out_dev) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  FilterGroups G;
+  DLSM_CHECK(filter_groups(block_key_end, block_end_offset, n_blocks, keys->n, bits_per_key, G));
+  if (out_len) *out_len = 0;
+  if (G.total > out_cap) return DLSM_E_CAPACITY;
+  DeviceGuard g(ctx->device);
+  // one legacy CreateFilter job per non-empty group, written in place
+  std::vector<dlsm_build_job> jobs;
+  for (size_t f = 0; f < G.off.size(); f++) {
+    if (G.end[f] == G.begin[f]) continue;
+    dlsm_build_job j{};
+    j.keys = *keys;
+    j.keys.n = G.end[f] - G.begin[f];
+    if (keys->offsets) j.keys.offsets = keys->offsets + G.begin[f];
+    else j.keys.bytes = keys->bytes + G.begin[f] * keys->key_len;
+    j.out = out_dev + G.off[f];
+    j.out_cap = legacy_bits(j.keys.n, bits_per_key) / 8 + 1;
+    jobs.push_back(j);
+  }
+  if (!jobs.empty()) {
+    DLSM_CHECK(ctx->st_len.ensure(jobs.size()));
+    DLSM_CHECK(dlsm_bloom_legacy_build_dev(ctx, jobs.data(), static_cast<int>(jobs.size()), bits_per_key,
+                                           ctx->st_len.p));
+  }
+  // Finish: Fixed32 filter offsets, Fixed32 array offset, kFilterBaseLg
+  std::vector<uint8_t> tail(G.total - G.array_offset);
+  for (size_t f = 0; f < G.off.size(); f++) memcpy(&tail[4 * f], &G.off[f], 4);  // little-endian
+  const uint32_t ao = static_cast<uint32_t>(G.array_offset);
+  memcpy(&tail[4 * G.off.size()], &ao, 4);
+  tail.back() = static_cast<uint8_t>(kFilterBaseLg);
+  DLSM_TRY(hipMemcpyAsync(out_dev + G.array_offset, tail.data(), tail.size(), hipMemcpyHostToDevice,
+                          ctx->stream));
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));  // `tail` is pageable host memory
+  if (out_len) *out_len = G.total;
+  return DLSM_OK;
+}
+
+int dlsm_filter_block_probe_dev(dlsm_ctx* ctx, const uint8_t* block_dev, uint64_t len,
+                                const dlsm_keyset* keys, const uint64_t* block_offsets_dev,
+                                uint8_t* out_dev) {
+  if (!ctx || !keys) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!out_dev || !block_offsets_dev || (len && !block_dev)) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  DLSM_TRY(launch_filter_block_probe(block_dev, len, to_desc(*keys), block_offsets_dev, out_dev, ctx->stream));
+  return DLSM_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Version: files + filters for the MultiGet-style probe (§8f row 3)
 // ---------------------------------------------------------------------------
 static_assert(DLSM_NUM_LEVELS == kNumLevels, "config::kNumLevels");

@@ -113,6 +113,8 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
 
 hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
                                 uint64_t* slot_mask, uint32_t* level_file, hipStream_t s);
+hipError_t launch_filter_block_probe(const uint8_t* blk, uint64_t len, KeyDesc keys,
+                                     const uint64_t* block_offsets, uint8_t* out, hipStream_t s);
 hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s, int n_jobs,
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,

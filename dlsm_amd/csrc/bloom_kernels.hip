@@ -1048,6 +1048,11 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
 // ---------------------------------------------------------------------------
 // Legacy FilterPolicy format (util/bloom.cc): global double hashing.
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dec32_dev(const uint8_t* p) {  // DecodeFixed32, any alignment
+  return static_cast<uint32_t>(p[0]) | (static_cast<uint32_t>(p[1]) << 8) |
+         (static_cast<uint32_t>(p[2]) << 16) | (static_cast<uint32_t>(p[3]) << 24);
+}
+
 __device__ __forceinline__ uint32_t legacy_bitpos(uint32_t h, uint64_t bits, uint32_t magic) {
   // bitpos = h % bits (size_t); for bits >= 2^32 that is h itself.
   return bits > 0xffffffffull ? h : fastmod(h, static_cast<uint32_t>(bits), magic);
@@ -1299,6 +1304,68 @@ hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snap
     version_probe_kernel<KM_K20><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
   else
     version_probe_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+  return hipGetLastError();
+}
+
+// FilterBlockReader::KeyMayMatch(block_offset, key), table/filter_block.cc:
+// 117-142, over one filter block (device), one thread per key.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void filter_block_probe_kernel(const uint8_t* __restrict__ blk,
+                                                                    uint64_t n, KeyDesc kd,
+                                                                    const uint64_t* __restrict__ offs,
+                                                                    uint8_t* __restrict__ out) {
+  const uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x;
+  if (i >= kd.n) return;
+  uint8_t r = 1;  // "Errors are treated as potential matches"
+  if (n >= 5) {
+    const uint32_t base_lg = blk[n - 1] & 63u;  // size_t(char) >> on x86: count mod 64
+    const uint32_t last_word = dec32_dev(blk + n - 5);
+    if (last_word <= n - 5) {
+      const uint64_t num = (n - 5 - last_word) / 4;
+      const uint64_t index = offs[i] >> base_lg;
+      if (index < num) {
+        const uint8_t* o = blk + last_word + index * 4;
+        const uint32_t start = dec32_dev(o), limit = dec32_dev(o + 4);
+        if (start <= limit && limit <= last_word) {
+          // BloomFilterPolicy::KeyMayMatch(key, filter), util/bloom.cc:57-81
+          const uint64_t len = limit - start;
+          const uint8_t* f = blk + start;
+          if (len < 2) {
+            r = 0;
+          } else {
+            const int k = static_cast<int>(static_cast<int8_t>(f[len - 1]));
+            if (k > 0 && k <= 30) {
+              const uint64_t bits = (len - 1) * 8;
+              uint32_t h = key_hash<MODE>(kd, i);
+              const uint32_t delta = bloom_delta(h);
+              for (int q = 0; q < k; q++) {
+                const uint32_t bp = bits > 0xffffffffull ? h : h % static_cast<uint32_t>(bits);
+                if (((f[bp >> 3] >> (bp & 7u)) & 1u) == 0) {
+                  r = 0;
+                  break;
+                }
+                h += delta;
+              }
+            }
+          }
+        } else if (start == limit) {
+          r = 0;  // empty filters do not match any keys
+        }
+      }
+    }
+  }
+  out[i] = r;
+}
+
+hipError_t launch_filter_block_probe(const uint8_t* blk, uint64_t len, KeyDesc keys,
+                                     const uint64_t* block_offsets, uint8_t* out, hipStream_t s) {
+  if (keys.n == 0) return hipSuccess;
+  const unsigned g = static_cast<unsigned>((keys.n + kBlock - 1) / kBlock);
+  if (keys.offsets == nullptr && keys.key_len == 20 && keys.suffix == 0 &&
+      (reinterpret_cast<uintptr_t>(keys.bytes) & 3u) == 0)
+    filter_block_probe_kernel<KM_K20><<<g, kBlock, 0, s>>>(blk, len, keys, block_offsets, out);
+  else
+    filter_block_probe_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(blk, len, keys, block_offsets, out);
   return hipGetLastError();
 }
 

@@ -299,6 +299,31 @@ int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64
 int dlsm_bloom_legacy_probe(dlsm_ctx* ctx, const uint8_t* filter, uint64_t len,
                             const dlsm_keyset* keys, uint8_t* out);
 
+/* ---- legacy block-based filter block (table/filter_block.cc) ------------ */
+
+/* FilterBlockBuilder (table/filter_block.cc:14-113) over one table, with the
+ * legacy BloomFilterPolicy: `keys` in table order; data block b holds keys
+ * [block_key_end[b-1], block_key_end[b]) and is followed by
+ * StartBlock(block_end_offset[b]) (TableBuilder::Flush).  A filter covers
+ * each 2 KiB (kFilterBaseLg = 11) of data-block offsets; keys after the last
+ * block end go to Finish's filter.  The block is the filters, Fixed32 offsets,
+ * Fixed32 array offset and the byte 11 -- bytes identical to Finish().
+ * dlsm_filter_block_size gives its length; build writes it to out_dev
+ * (device) and sets *out_len (host).  Synchronous. */
+int dlsm_filter_block_size(const uint64_t* block_key_end, const uint64_t* block_end_offset,
+                           int n_blocks, uint64_t n_keys, int bits_per_key, uint64_t* nbytes);
+int dlsm_filter_block_build_dev(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64_t* block_key_end,
+                                const uint64_t* block_end_offset, int n_blocks, int bits_per_key,
+                                uint8_t* out_dev, uint64_t out_cap, uint64_t* out_len);
+
+/* FilterBlockReader::KeyMayMatch(block_offset, key) (filter_block.cc:117-142)
+ * for every key against one filter block (device): out_dev[i] = 0/1 for key i
+ * in the data block at block_offsets_dev[i] (device u64).  Malformed blocks
+ * answer 1 ("errors are treated as potential matches").  Asynchronous. */
+int dlsm_filter_block_probe_dev(dlsm_ctx* ctx, const uint8_t* block_dev, uint64_t len,
+                                const dlsm_keyset* keys, const uint64_t* block_offsets_dev,
+                                uint8_t* out_dev);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -60,6 +60,11 @@ def lib():
                                                C.c_uint64, u8p, u64p]
         L.orc_version_probe.argtypes = [C.c_void_p, C.c_int, u8p, u64p, C.c_uint32, C.c_uint32,
                                         C.c_uint64, C.c_uint64, u64p, C.POINTER(C.c_uint32)]
+        L.orc_filter_block_build.restype = C.c_int64
+        L.orc_filter_block_build.argtypes = [u8p, u64p, C.c_uint32, C.c_uint64, u64p, u64p, C.c_int,
+                                             C.c_int, C.c_int, u8p, C.c_uint64]
+        L.orc_filter_block_key_may_match.argtypes = [u8p, C.c_uint64, C.c_uint64, u8p, C.c_size_t,
+                                                     C.c_int]
         L.orc_full_reader_parse.argtypes = [u8p, C.c_uint64, C.POINTER(C.c_int),
                                             C.POINTER(C.c_uint32), C.POINTER(C.c_int)]
         L.orc_full_key_may_match.argtypes = [u8p, C.c_uint64, u8p, C.c_size_t]
@@ -229,6 +234,28 @@ def version_probe(files, keys: np.ndarray, n: int, snapshot: int, stride: int = 
                                  snapshot, _ptr(mask, u64p), lf.ctypes.data_as(C.POINTER(C.c_uint32)))
     assert st == 0, st
     return mask[:n], lf[:n]
+
+
+def filter_block_build(keys: np.ndarray, n: int, block_key_end, block_end_offset,
+                       stride: int = 20, offsets=None, policy: int = 0, bpk: int = 10) -> bytes:
+    """FilterBlockBuilder driven like TableBuilder (orc_filter_block_build).
+    policy 0 = BloomFilterPolicy, 1 = filter_block_test.cc's TestHashFilter."""
+    ke = np.asarray(block_key_end, dtype=np.uint64)
+    eo = np.asarray(block_end_offset, dtype=np.uint64)
+    cap = 64 + 8 * (len(ke) + int(eo.max() // 2048 if len(eo) else 0) + 2) + 16 * n + n * bpk // 8 * 2 + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    r = lib().orc_filter_block_build(_ptr(keys), _ptr(offsets, u64p), stride, n, _ptr(ke, u64p),
+                                     _ptr(eo, u64p), len(ke), policy, bpk, _ptr(out), cap)
+    if r < 0:
+        raise ValueError(f"orc_filter_block_build: {r}")
+    return out[:r].tobytes()
+
+
+def filter_block_key_may_match(block: bytes, block_offset: int, key: bytes, policy: int = 0) -> int:
+    b = np.frombuffer(block + b"\0", dtype=np.uint8)
+    k = np.frombuffer(key + b"\0", dtype=np.uint8)
+    return lib().orc_filter_block_key_may_match(_ptr(b), len(block), block_offset, _ptr(k), len(key),
+                                                policy)
 
 
 def full_reader_parse(filt: bytes):

@@ -699,3 +699,113 @@ int orc_version_probe(const orc_version_file* files, int n_files, const uint8_t*
   }
   return 0;
 }
+
+/* ------------------------------------------------------------------------
+ * Legacy block-based filter block, restated: FilterBlockBuilder /
+ * FilterBlockReader (table/filter_block.cc:14-142) driven the way
+ * TableBuilder drives it -- the keys of data block b are AddKey'ed, then
+ * StartBlock(block_end_offset[b]) runs (TableBuilder::Flush); keys past the
+ * last block end are added before Finish().
+ * policy 0 = BloomFilterPolicy(bits_per_key) (util/bloom.cc);
+ * policy 1 = TestHashFilter of table/filter_block_test.cc:17-36 (one
+ * Fixed32(Hash(key, 1)) per key), so that file's expectations apply verbatim.
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t* result; uint64_t size, cap;           /* Slice result */
+  uint32_t* offs; uint64_t n_offs, cap_offs;     /* filter_offsets_ */
+  uint64_t key_begin, key_end;                   /* start_: pending keys [begin, end) */
+  const uint8_t* bytes; const uint64_t* offsets; uint32_t stride;
+  int policy, bpk, err;
+} orc_fbb;
+
+static void fbb_put32(orc_fbb* b, uint32_t v) {
+  if (b->size + 4 > b->cap) { b->err = 1; return; }
+  enc32(b->result + b->size, v);
+  b->size += 4;
+}
+
+static void fbb_generate(orc_fbb* b) { /* GenerateFilter */
+  if (b->n_offs == b->cap_offs) { b->err = 1; return; }
+  const uint64_t num_keys = b->key_end - b->key_begin;
+  b->offs[b->n_offs++] = (uint32_t)b->size; /* both paths push result.size() first */
+  if (num_keys == 0) return;                /* fast path */
+  if (b->policy == 0) {
+    /* CreateFilter on the flattened sub-range (keys re-based like tmp_keys_) */
+    const uint64_t need = orc_legacy_filter_bytes(num_keys, b->bpk);
+    if (b->size + need > b->cap) { b->err = 1; return; }
+    const uint8_t* base = b->offsets ? b->bytes : b->bytes + b->key_begin * b->stride;
+    const uint64_t* offs = b->offsets ? b->offsets + b->key_begin : NULL;
+    orc_legacy_build(base, offs, b->stride, num_keys, b->bpk, b->result + b->size, need);
+    b->size += need;
+  } else {
+    for (uint64_t i = b->key_begin; i < b->key_end; i++) {
+      size_t len;
+      const uint8_t* k = key_at(b->bytes, b->offsets, b->stride, i, &len);
+      fbb_put32(b, orc_hash(k, len, 1));
+    }
+  }
+  b->key_begin = b->key_end;
+}
+
+static void fbb_start_block(orc_fbb* b, uint64_t block_offset) { /* StartBlock */
+  const uint64_t filter_index = block_offset / 2048; /* kFilterBase = 1 << 11 */
+  if (filter_index < b->n_offs) { b->err = 2; return; } /* assert */
+  while (filter_index > b->n_offs && !b->err) fbb_generate(b);
+}
+
+int64_t orc_filter_block_build(const uint8_t* bytes, const uint64_t* offsets, uint32_t stride,
+                               uint64_t n, const uint64_t* block_key_end,
+                               const uint64_t* block_end_offset, int n_blocks, int policy,
+                               int bits_per_key, uint8_t* out, uint64_t out_cap) {
+  orc_fbb b;
+  memset(&b, 0, sizeof(b));
+  b.result = out; b.cap = out_cap;
+  b.cap_offs = 1 << 22;
+  b.offs = (uint32_t*)malloc(sizeof(uint32_t) * b.cap_offs);
+  b.bytes = bytes; b.offsets = offsets; b.stride = stride; b.policy = policy; b.bpk = bits_per_key;
+  if (!b.offs) return ORC_E_ARG;
+  uint64_t next = 0;
+  for (int blk = 0; blk < n_blocks && !b.err; blk++) {
+    for (; next < block_key_end[blk]; next++) b.key_end = next + 1; /* AddKey */
+    fbb_start_block(&b, block_end_offset[blk]);
+  }
+  for (; next < n; next++) b.key_end = next + 1;
+  if (!b.err && b.key_end > b.key_begin) fbb_generate(&b); /* Finish: start_ not empty */
+  const uint32_t array_offset = (uint32_t)b.size;
+  for (uint64_t i = 0; i < b.n_offs && !b.err; i++) fbb_put32(&b, b.offs[i]);
+  fbb_put32(&b, array_offset);
+  if (!b.err && b.size + 1 <= b.cap) b.result[b.size++] = 11; /* kFilterBaseLg */
+  else b.err = b.err ? b.err : 1;
+  free(b.offs);
+  if (b.err) return b.err == 2 ? ORC_E_ARG : ORC_E_CAPACITY;
+  return (int64_t)b.size;
+}
+
+/* FilterBlockReader ctor + KeyMayMatch(block_offset, key). */
+int orc_filter_block_key_may_match(const uint8_t* contents, uint64_t n, uint64_t block_offset,
+                                   const uint8_t* key, size_t klen, int policy) {
+  if (n < 5) return 1; /* data_ == nullptr, num_ == 0 -> "potential match" */
+  const uint64_t base_lg = (uint64_t)(int64_t)(int8_t)contents[n - 1];
+  const uint32_t last_word = dec32(contents + n - 5);
+  if (last_word > n - 5) return 1;
+  const uint8_t* data = contents;
+  const uint8_t* offset = data + last_word;
+  const uint64_t num = (n - 5 - last_word) / 4;
+  const uint64_t index = block_offset >> (base_lg & 63); /* x86 shr: count mod 64 */
+  if (index < num) {
+    const uint32_t start = dec32(offset + index * 4);
+    const uint32_t limit = dec32(offset + index * 4 + 4);
+    if (start <= limit && limit <= (uint64_t)(offset - data)) {
+      const uint8_t* f = data + start;
+      const uint64_t flen = limit - start;
+      if (policy == 0) return orc_legacy_key_may_match(f, flen, key, klen);
+      const uint32_t h = orc_hash(key, klen, 1);
+      for (uint64_t i = 0; i + 4 <= flen; i += 4)
+        if (h == dec32(f + i)) return 1;
+      return 0;
+    } else if (start == limit) {
+      return 0;
+    }
+  }
+  return 1;
+}
