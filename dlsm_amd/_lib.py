@@ -91,6 +91,9 @@ SIGNATURES = [
     ("dlsm_filter_block_build_dev", C.c_int, [_VP, C.POINTER(dlsm_keyset), _VP, _VP, C.c_int,
                                               C.c_int, _VP, C.c_uint64, _U64P]),
     ("dlsm_filter_block_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP, _VP]),
+    ("dlsm_filter_block_build", C.c_int, [_VP, C.POINTER(dlsm_keyset), _VP, _VP, C.c_int, C.c_int,
+                                          _VP, C.c_uint64, _U64P]),
+    ("dlsm_filter_block_probe", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP, _VP]),
     ("dlsm_version_create", C.c_int, [_VP, C.POINTER(dlsm_version_file), C.c_int, C.c_int,
                                       C.POINTER(_VP)]),
     ("dlsm_version_destroy", C.c_int, [_VP]),

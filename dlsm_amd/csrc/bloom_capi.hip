@@ -1099,6 +1099,54 @@ int dlsm_filter_block_probe_dev(dlsm_ctx* ctx, const uint8_t* block_dev, uint64_
   return DLSM_OK;
 }
 
+int dlsm_filter_block_build(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64_t* block_key_end,
+                            const uint64_t* block_end_offset, int n_blocks, int bits_per_key,
+                            uint8_t* out, uint64_t out_cap, uint64_t* out_len) {
+  if (!ctx || !keys || !out) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  uint64_t need = 0;
+  DLSM_CHECK(dlsm_filter_block_size(block_key_end, block_end_offset, n_blocks, keys->n, bits_per_key, &need));
+  if (out_len) *out_len = 0;
+  if (need > out_cap) return DLSM_E_CAPACITY;
+  DeviceGuard g(ctx->device);
+  const dlsm_keyset* sets[1] = {keys};
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets, 1, dk));
+  DLSM_CHECK(ctx->st_out.ensure(need));
+  uint64_t len = 0;
+  DLSM_CHECK(dlsm_filter_block_build_dev(ctx, &dk[0], block_key_end, block_end_offset, n_blocks,
+                                         bits_per_key, ctx->st_out.p, need, &len));
+  DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p, len, hipMemcpyDeviceToHost, ctx->stream));
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  if (out_len) *out_len = len;
+  return DLSM_OK;
+}
+
+int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, const dlsm_keyset* keys,
+                            const uint64_t* block_offsets, uint8_t* out) {
+  if (!ctx || !keys) return DLSM_E_ARG;
+  DLSM_CHECK(validate_keyset(*keys));
+  if (keys->n == 0) return DLSM_OK;
+  if (!out || !block_offsets || (len && !block)) return DLSM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  const dlsm_keyset* sets[1] = {keys};
+  std::vector<dlsm_keyset> dk;
+  DLSM_CHECK(stage_keys(ctx, sets, 1, dk));
+  // staging: [block | offsets | answers]
+  const uint64_t bo = (len + 15) & ~uint64_t(15);
+  const uint64_t oo = bo + 8 * keys->n;
+  DLSM_CHECK(ctx->st_out.ensure(oo + keys->n));
+  if (len) DLSM_TRY(hipMemcpyAsync(ctx->st_out.p, block, len, hipMemcpyHostToDevice, s));
+  DLSM_TRY(hipMemcpyAsync(ctx->st_out.p + bo, block_offsets, 8 * keys->n, hipMemcpyHostToDevice, s));
+  DLSM_CHECK(dlsm_filter_block_probe_dev(ctx, len ? ctx->st_out.p : nullptr, len, &dk[0],
+                                         reinterpret_cast<const uint64_t*>(ctx->st_out.p + bo),
+                                         ctx->st_out.p + oo));
+  DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p + oo, keys->n, hipMemcpyDeviceToHost, s));
+  DLSM_TRY(hipStreamSynchronize(s));
+  return DLSM_OK;
+}
+
 // ---------------------------------------------------------------------------
 // Version: files + filters for the MultiGet-style probe (§8f row 3)
 // ---------------------------------------------------------------------------

@@ -323,6 +323,13 @@ int dlsm_filter_block_build_dev(dlsm_ctx* ctx, const dlsm_keyset* keys, const ui
 int dlsm_filter_block_probe_dev(dlsm_ctx* ctx, const uint8_t* block_dev, uint64_t len,
                                 const dlsm_keyset* keys, const uint64_t* block_offsets_dev,
                                 uint8_t* out_dev);
+/* Host-memory forms of the two calls above (keys, block, offsets, outputs on
+ * the host; staged through device memory).  Synchronous. */
+int dlsm_filter_block_build(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64_t* block_key_end,
+                            const uint64_t* block_end_offset, int n_blocks, int bits_per_key,
+                            uint8_t* out, uint64_t out_cap, uint64_t* out_len);
+int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, const dlsm_keyset* keys,
+                            const uint64_t* block_offsets, uint8_t* out);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -9,6 +9,10 @@
 //       ctor parses metadata; KeyMayMatch; + KeysMayMatch (batch)
 //   BloomFilterPolicy       include/TimberSaw/filter_policy.h:31-55, util/bloom.cc
 //       Name / CreateFilter / KeyMayMatch
+//   FilterBlockBuilder      table/filter_block.h:34-68 (legacy 2 KiB framing)
+//       StartBlock AddKey* ... Finish; public `result`
+//   FilterBlockReader       table/filter_block.h:70-85
+//       KeyMayMatch(block_offset, key) + KeysMayMatch (batch)
 //
 // No exceptions (the reference builds with -fno-exceptions): failures are
 // reported through status().  All compute runs on the GPU behind the ABI.
@@ -214,6 +218,77 @@ class BloomFilterPolicy {
   int bits_per_key_;
   dlsm_ctx* ctx_;
   mutable int last_status_ = DLSM_OK;
+};
+
+// table/filter_block.cc:14-113 with the legacy Bloom policy.  StartBlock /
+// AddKey only record the call sequence; Finish builds every filter of the
+// block on the GPU and writes the block (filters, offsets, array offset,
+// kFilterBaseLg) into the slot.
+class FilterBlockBuilder {
+ public:
+  FilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx)
+      : local_mr_(mr), bits_per_key_(bits_per_key), ctx_(ctx), result(static_cast<char*>(mr->addr), 0) {
+    offsets_.push_back(0);
+  }
+  FilterBlockBuilder(const FilterBlockBuilder&) = delete;
+  FilterBlockBuilder& operator=(const FilterBlockBuilder&) = delete;
+
+  void StartBlock(uint64_t block_offset) {
+    block_key_end_.push_back(offsets_.size() - 1);
+    block_end_offset_.push_back(block_offset);
+  }
+  void AddKey(const Slice& key) {
+    keys_.append(key.data(), key.size());
+    offsets_.push_back(keys_.size());
+  }
+  Slice Finish() {
+    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(keys_.data()), offsets_.data(), 0, 0,
+                   offsets_.size() - 1};
+    uint64_t len = 0;
+    status_ = dlsm_filter_block_build(ctx_, &ks, block_key_end_.data(), block_end_offset_.data(),
+                                      static_cast<int>(block_key_end_.size()), bits_per_key_,
+                                      reinterpret_cast<uint8_t*>(local_mr_->addr), local_mr_->length, &len);
+    result.Reset(static_cast<char*>(local_mr_->addr), status_ == DLSM_OK ? len : 0);
+    return result;
+  }
+  void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
+  int status() const { return status_; }
+
+  Slice result;
+
+ private:
+  FilterSlot* local_mr_;
+  int bits_per_key_;
+  dlsm_ctx* ctx_;
+  std::string keys_;
+  std::vector<uint64_t> offsets_;
+  std::vector<uint64_t> block_key_end_, block_end_offset_;
+  int status_ = DLSM_OK;
+};
+
+class FilterBlockReader {
+ public:
+  FilterBlockReader(const Slice& contents, dlsm_ctx* ctx) : contents_(contents), ctx_(ctx) {}
+  bool KeyMayMatch(uint64_t block_offset, const Slice& key) {
+    uint8_t m = 0;
+    return KeysMayMatch(&block_offset, &key, 1, &m) == DLSM_OK && m != 0;
+  }
+  int KeysMayMatch(const uint64_t* block_offsets, const Slice* keys, size_t n, uint8_t* out) {
+    std::string bytes;
+    std::vector<uint64_t> offs(1, 0);
+    for (size_t i = 0; i < n; i++) {
+      bytes.append(keys[i].data(), keys[i].size());
+      offs.push_back(bytes.size());
+    }
+    if (bytes.empty()) bytes.push_back('\0');
+    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0, n};
+    return dlsm_filter_block_probe(ctx_, reinterpret_cast<const uint8_t*>(contents_.data()),
+                                   contents_.size(), &ks, block_offsets, out);
+  }
+
+ private:
+  Slice contents_;
+  dlsm_ctx* ctx_;
 };
 
 }  // namespace dlsm_adapter

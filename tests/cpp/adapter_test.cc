@@ -14,6 +14,9 @@ int orc_full_key_may_match(const uint8_t*, uint64_t, const uint8_t*, size_t);
 int64_t orc_legacy_build(const uint8_t*, const uint64_t*, uint32_t, uint64_t, int, uint8_t*, uint64_t);
 int orc_legacy_key_may_match(const uint8_t*, uint64_t, const uint8_t*, size_t);
 void orc_dbbench_key(uint64_t v, int key_size, uint8_t* out);
+int64_t orc_filter_block_build(const uint8_t*, const uint64_t*, uint32_t, uint64_t, const uint64_t*,
+                               const uint64_t*, int, int, int, uint8_t*, uint64_t);
+int orc_filter_block_key_may_match(const uint8_t*, uint64_t, uint64_t, const uint8_t*, size_t, int);
 }
 
 #define CHECK(c)                                                   \
@@ -112,6 +115,51 @@ int main() {
       CHECK(pol.KeyMayMatch(Slice(q, std::strlen(q)), filt) ==
             (orc_legacy_key_may_match(want.data(), wl, reinterpret_cast<const uint8_t*>(q),
                                       std::strlen(q)) != 0));
+  }
+  // ---- FilterBlockBuilder / FilterBlockReader: TableBuilder's call shape
+  // (StartBlock after each data block flush, filter_block.cc:32-38) ----
+  {
+    std::vector<char> slot(64 * 1024, 0);
+    dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+    dlsm_adapter::FilterBlockBuilder fb(&mr, 10, ctx);
+    std::vector<std::string> ks;
+    std::vector<uint64_t> ke, eo, key_block;
+    uint64_t off = 0;
+    fb.StartBlock(0);  // TableBuilder ctor
+    ke.push_back(0);
+    eo.push_back(0);
+    for (int b = 0; b < 40; b++) {
+      for (int i = 0; i < 7 + (b * 5) % 13; i++) {
+        char k[20];
+        orc_dbbench_key(1000 * b + i, 20, reinterpret_cast<uint8_t*>(k));
+        ks.emplace_back(k, 20);
+        key_block.push_back(off);
+        fb.AddKey(Slice(ks.back()));
+      }
+      off += 700 + 211 * (b % 9);
+      fb.StartBlock(off);  // TableBuilder::Flush
+      ke.push_back(ks.size());
+      eo.push_back(off);
+    }
+    Slice blk = fb.Finish();
+    CHECK(fb.status() == DLSM_OK);
+    std::string flat;
+    std::vector<uint64_t> offs{0};
+    for (auto& s : ks) {
+      flat += s;
+      offs.push_back(flat.size());
+    }
+    std::vector<uint8_t> want(64 * 1024, 0);
+    int64_t wl = orc_filter_block_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0,
+                                        ks.size(), ke.data(), eo.data(), static_cast<int>(ke.size()), 0,
+                                        10, want.data(), want.size());
+    CHECK(wl > 0 && static_cast<int64_t>(blk.size()) == wl);
+    CHECK(std::memcmp(blk.data(), want.data(), wl) == 0);
+    dlsm_adapter::FilterBlockReader rd(blk, ctx);
+    for (size_t i = 0; i < ks.size(); i += 3)
+      CHECK(rd.KeyMayMatch(key_block[i], Slice(ks[i])) ==
+            (orc_filter_block_key_may_match(want.data(), wl, key_block[i],
+                                            reinterpret_cast<const uint8_t*>(ks[i].data()), 20, 0) != 0));
   }
   dlsm_ctx_destroy(ctx);
   std::printf("OK adapter\n");
