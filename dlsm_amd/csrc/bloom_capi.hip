@@ -402,9 +402,13 @@ int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   DeviceGuard g(ctx->device);
   // probe intermediates are sized in whole chunks of up to 2^14 keys
   const uint64_t pkeys = (max_keys + 16383u) & ~uint64_t(16383u);
-  DLSM_CHECK(ctx->entries.ensure(pkeys));
+  // probe entries / answers: chunk regions of probe_region(C) per C keys
+  uint64_t pregion = 0;
+  for (uint32_t C : {4096u, 8192u, 16384u})
+    pregion = std::max<uint64_t>(pregion, ((max_keys + C - 1) / C) * probe_region(C));
+  DLSM_CHECK(ctx->entries.ensure(std::max(pkeys, pregion)));
   DLSM_CHECK(ctx->pos.ensure(pkeys));
-  DLSM_CHECK(ctx->smask.ensure(pkeys));
+  DLSM_CHECK(ctx->smask.ensure(pregion));
   const uint64_t chunks = (max_keys + kBuildChunk - 1) / kBuildChunk + max_jobs;
   DLSM_CHECK(ctx->tab.ensure(chunks * (kMaxSlices + 1)));
   DLSM_CHECK(ctx->jobs.ensure(max_jobs));
@@ -939,10 +943,11 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   const int nbuf = pipe ? kProbeBufs : 1;
   const uint32_t nCmax = ceil_div_u32(std::min(round, n), C);
   const uint64_t kstride = static_cast<uint64_t>(nCmax) * C;  // keys per buffer (16-B aligned)
+  const uint64_t rstride = static_cast<uint64_t>(nCmax) * probe_region(static_cast<uint32_t>(C));  // entries / answers
   const uint64_t tstride = static_cast<uint64_t>(S + 1) * nCmax;        // table u16 per buffer
-  DLSM_CHECK(ctx->entries.ensure(kstride * nbuf));
+  DLSM_CHECK(ctx->entries.ensure(rstride * nbuf));
   DLSM_CHECK(ctx->pos.ensure(kstride * nbuf));
-  DLSM_CHECK(ctx->smask.ensure(kstride * nbuf));
+  DLSM_CHECK(ctx->smask.ensure(rstride * nbuf));
   DLSM_CHECK(ctx->tab.ensure(tstride * nbuf));
   if (pipe) DLSM_CHECK(fork_aux(ctx));
   hipStream_t ps = pipe ? ctx->aux : s;
@@ -951,9 +956,9 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     const uint64_t nr = std::min(round, n - r0);
     const uint32_t nC = ceil_div_u32(nr, C);
     const int b = static_cast<int>(r % nbuf);
-    uint32_t* ent = ctx->entries.p + b * kstride;
+    uint32_t* ent = ctx->entries.p + b * rstride;
     uint16_t* pos = ctx->pos.p + b * kstride;
-    uint8_t* sm = ctx->smask.p + b * kstride;
+    uint8_t* sm = ctx->smask.p + b * rstride;
     uint16_t* tab = ctx->tab.p + b * tstride;
     KeyDesc kr = kd;
     kr.n = nr;
@@ -962,7 +967,13 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     // (slice, part) workgroups: about one resident wave of workgroups (256
     // CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at least one
     // 64-chunk group per wave.
-    const uint32_t resident = lgR == 7 ? 512u : 256u;
+    // ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU: a tuning knob
+    // for the pipelined rounds, where a partition workgroup shares each CU)
+    static const uint32_t per_cu_env = [] {
+      const char* e = getenv("DLSM_SLICE_WGS_PER_CU");
+      return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+    }();
+    const uint32_t resident = 256u * (per_cu_env ? per_cu_env : (lgR == 7 ? 2u : 1u));
     int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
     parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 1024)));
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));

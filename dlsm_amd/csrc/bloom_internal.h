@@ -76,6 +76,9 @@ constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
 constexpr int kBuildChunk = 4096;   // keys per partition chunk (build)
 constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
+// u32 entries (and answer bytes) per probe chunk region: C keys plus up to 3
+// padding entries per slice bucket (buckets are padded to 16-byte units).
+constexpr uint32_t probe_region(uint32_t C) { return C + 4u * kMaxSlices; }
 
 // ---- launchers (bloom_kernels.hip) -----------------------------------------
 // All return the hipError_t of the launch.  `dchunk` holds one

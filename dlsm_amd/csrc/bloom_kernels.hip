@@ -402,8 +402,12 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 // wave keeps a set of loads in flight while it works on the previous one --
 // the un-pipelined walk spent most of its cycles waiting on these loads.
 // act(hv[U], idx[U], ok[U], g) consumes one window set of group g.
-template <int U, uint32_t CHUNK>
+// E: the walk's element -- uint32_t (one entry) or uint4 (a 16-byte unit of
+// four entries, for bucket offsets that are multiples of 4); CHUNK: a
+// chunk region's stride in elements.
+template <int U, uint32_t CHUNK, typename E = uint32_t>
 struct SegWalk {
+  static constexpr uint32_t kPerE = sizeof(E) / 4;  // entries per element
   const uint16_t* tb;
   const uint32_t* entries;
   uint32_t rowlen, g_step, g_end;
@@ -411,17 +415,20 @@ struct SegWalk {
   uint32_t e0;        // next window start in the current group
   uint32_t excl, dv, T;
   uint64_t nz;        // non-empty segments of the current group
-  uint32_t n0, n1;    // prefetched table row of group g + g_step (this lane's chunk)
+  uint32_t nrow;      // prefetched table row pair of group g + g_step (this lane's chunk), packed
 
-  __device__ __forceinline__ void load_rows(uint32_t gg, uint32_t& a0, uint32_t& a1) const {
+  // The row pair (bucket start, bucket end) of this lane's chunk as one
+  // packed u32, unpacked only in setup(): the load stays in flight until the
+  // next group starts instead of being waited on where it is issued.
+  __device__ __forceinline__ uint32_t load_rows(uint32_t gg) const {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = min(gg + lane, g_end - 1u);  // clamped: unconditional loads
     const uint16_t* r = tb + static_cast<uint64_t>(c) * rowlen;
-    a0 = r[0];
-    a1 = r[1];
+    return static_cast<uint32_t>(r[0]) | (static_cast<uint32_t>(r[1]) << 16);
   }
-  __device__ __forceinline__ void setup(uint32_t a0, uint32_t a1) {
+  __device__ __forceinline__ void setup(uint32_t row) {
     const uint32_t lane = threadIdx.x & 63;
+    const uint32_t a0 = (row & 0xffffu) / kPerE, a1 = (row >> 16) / kPerE;
     const uint32_t cnt = g + lane < g_end ? a1 - a0 : 0u;
     const uint32_t incl = wave_incl_scan_dpp(cnt);
     excl = incl - cnt;
@@ -433,10 +440,9 @@ struct SegWalk {
   __device__ __forceinline__ bool start(uint32_t g_first) {
     g = g_first;
     if (g >= g_end) return false;
-    uint32_t a0, a1;
-    load_rows(g, a0, a1);
-    if (g + g_step < g_end) load_rows(g + g_step, n0, n1);
-    setup(a0, a1);
+    const uint32_t row = load_rows(g);
+    if (g + g_step < g_end) nrow = load_rows(g + g_step);
+    setup(row);
     return true;
   }
   // Locate the next window set; false when the walk is done.
@@ -444,45 +450,60 @@ struct SegWalk {
     while (e0 >= T) {
       g += g_step;
       if (g >= g_end) return false;
-      const uint32_t a0 = n0, a1 = n1;
-      if (g + g_step < g_end) load_rows(g + g_step, n0, n1);
-      setup(a0, a1);
+      const uint32_t row = nrow;
+      if (g + g_step < g_end) nrow = load_rows(g + g_step);
+      setup(row);
     }
     seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
     e0 += kWin * U;
     gset = g;
     return true;
   }
-  __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, uint32_t (&hv)[U]) const {
-    const uint32_t* gent = entries + static_cast<uint64_t>(gset) * CHUNK;
+  __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
+    const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
 #pragma unroll
     for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
   }
 };
 
-template <int U, uint32_t CHUNK, typename Act>
+// Window sets in flight per wave: set i+DEPTH's loads are issued before set i
+// is consumed.  DEPTH 2 keeps two sets of loads in flight (the walk of a
+// U = 1 unit window is short next to a loaded HBM round trip).
+template <int U, uint32_t CHUNK, typename E>
+struct WinSet {
+  uint32_t idx[U], g;
+  E hv[U];
+  bool ok[U];
+};
+
+template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, typename Act>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, Act act) {
-  SegWalk<U, CHUNK> w{tb, entries, rowlen, g_step, g_end};
+  static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
+  SegWalk<U, CHUNK, E> w{tb, entries, rowlen, g_step, g_end};
   if (!w.start(g_first)) return;
-  uint32_t idxA[U], hvA[U], gA;
-  bool okA[U];
-  if (!w.next(idxA, okA, gA)) return;
-  w.fetch(idxA, gA, hvA);
+  WinSet<U, CHUNK, E> A, B;
+  if (!w.next(A.idx, A.ok, A.g)) return;
+  w.fetch(A.idx, A.g, A.hv);
+  bool haveB = false;
+  if constexpr (DEPTH == 2) {
+    haveB = w.next(B.idx, B.ok, B.g);
+    if (haveB) w.fetch(B.idx, B.g, B.hv);
+  }
   while (true) {
-    uint32_t idxB[U], hvB[U], gB;
-    bool okB[U];
-    const bool more = w.next(idxB, okB, gB);
-    if (more) w.fetch(idxB, gB, hvB);
-    act(hvA, idxA, okA, gA);
-    if (!more) break;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      idxA[u] = idxB[u];
-      hvA[u] = hvB[u];
-      okA[u] = okB[u];
+    WinSet<U, CHUNK, E> N;
+    const bool more = (DEPTH == 1 || haveB) && w.next(N.idx, N.ok, N.g);
+    if (more) w.fetch(N.idx, N.g, N.hv);
+    act(A.hv, A.idx, A.ok, A.g);
+    if constexpr (DEPTH == 1) {
+      if (!more) break;
+      A = N;
+    } else {
+      if (!haveB) break;
+      A = B;
+      B = N;
+      haveB = more;
     }
-    gA = gB;
   }
 }
 
@@ -598,7 +619,13 @@ constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
 // probe slices: 64 KiB LDS per workgroup, 512 or 1024 threads (launch_probe_slices)
 constexpr int kWalkU = 8;               // hashes in flight per lane (build segment walk)
 #ifndef DLSM_PROBE_U
-#define DLSM_PROBE_U 4
+#define DLSM_PROBE_U 1
+#endif
+#ifndef DLSM_PROBE_DEPTH
+#define DLSM_PROBE_DEPTH 1  // window sets of loads in flight per wave (walk_segments)
+#endif
+#ifndef DLSM_PROBE_NT
+#define DLSM_PROBE_NT 1024  // probe slice workgroup size (two 64 KiB slices per CU)
 #endif
 #ifndef DLSM_PROBE_MINWAVES
 #define DLSM_PROBE_MINWAVES 1
@@ -803,29 +830,37 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
 // in the unused bits [9, 17), so the slice pass needs no modulo: the LDS base
 // of the key's line is `e & kEntryLineMask` (= offset * 512) and the
 // positions are (e + q * (e >> 17)) & 511, exactly those of h.
+// Bit 31 is never read either: valid entries clear it, and the bucket
+// padding is kProbePadEntry (bit 31 set; its answer byte is never read).
 constexpr uint32_t kEntryLineMask = 0xffu << 9;
+constexpr uint32_t kProbePadEntry = 0x80000000u;
 __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
-  return (h & ~kEntryLineMask) | (line_off << 9);
+  return (h & ~(kEntryLineMask | kProbePadEntry)) | (line_off << 9);
 }
 
 // Pass 1: hash each lookup once and bucket it by slice inside its chunk.
-// entries[chunk region] = packed entries (probe_entry) grouped by slice;
-// pos[i] = where key i went.
-// NT threads per chunk of C keys (C/NT keys per thread).
+// entries[chunk region of probe_region(C) u32] = packed entries (probe_entry)
+// grouped by slice, every bucket padded to a multiple of 4 entries with
+// kProbePadEntry, so the slice pass moves whole 16-byte units; pos[i] = where
+// key i went.  NT threads per chunk of C keys (C/NT keys per thread).
 template <int MODE, int NT, int C>
 __global__ __launch_bounds__(NT) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
   constexpr int PER = C / NT;
-  // the key tile doubles as the bucketed-hash staging area (C u32)
-  constexpr int TV = K20Tile<NT, kTileKPT>::kVec > C / 4 ? K20Tile<NT, kTileKPT>::kVec : C / 4;
-  static_assert(PER % kTileKPT == 0 && C <= 65536, "chunk shape");
+  constexpr uint32_t CR = probe_region(C);
+  // the key tile doubles as the bucketed-entry staging area (CR u32)
+  constexpr int TV = K20Tile<NT, kTileKPT>::kVec > static_cast<int>(CR / 4) ? K20Tile<NT, kTileKPT>::kVec
+                                                                           : static_cast<int>(CR / 4);
+  static_assert(PER % kTileKPT == 0 && CR <= 65536, "chunk shape");
   __shared__ __attribute__((aligned(16))) uint4 tile[TV];
   __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
   __shared__ uint8_t sb[C];                                // slice (S <= 256)
   __shared__ uint32_t hist[kMaxSlices + 1];
+  __shared__ uint8_t npad[kMaxSlices + 1];
   __shared__ uint32_t wsum[NT / 64];
   const int tid = threadIdx.x;
+  uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
   for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
     const uint64_t first = static_cast<uint64_t>(c) * C;
@@ -846,10 +881,22 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
       }
     }
     __syncthreads();
-    block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
+    for (uint32_t b = tid; b < S; b += NT) {  // pad every bucket to whole 16-byte units
+      const uint32_t pad = (0u - hist[b]) & 3u;
+      npad[b] = static_cast<uint8_t>(pad);
+      hist[b] += pad;
+    }
+    __syncthreads();
+    const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
     for (uint32_t b = tid; b <= S; b += NT)
       tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);  // one row per chunk
-    uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
+    for (uint32_t b = tid; b < S; b += NT) {
+      const uint32_t end = hist[b + 1];
+      const uint32_t np = npad[b];
+      if (np > 0) stage[end - 1] = kProbePadEntry;
+      if (np > 1) stage[end - 2] = kProbePadEntry;
+      if (np > 2) stage[end - 3] = kProbePadEntry;
+    }
 #pragma unroll
     for (int r = 0; r < PER; r++) {
       const uint32_t i = r * NT + tid;
@@ -860,8 +907,8 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
       }
     }
     __syncthreads();
-    // coalesced 16-byte stores of the bucketed hashes and of the positions
-    store_chunk_u32<NT>(entries + first, stage, nk);
+    // coalesced 16-byte stores of the bucketed entries and of the positions
+    store_chunk_u32<NT>(entries + static_cast<uint64_t>(c) * CR, stage, total);
     store_chunk_u16<NT>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
   }
@@ -904,36 +951,52 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
   __syncthreads();
-  walk_segments<U, C>(
+  constexpr uint32_t CRU = probe_region(C) / 4;  // chunk region stride in 16-byte units
+  // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
+  // window, probes its 4 entries and writes their 4 answer bytes as one dword
+  // (the answers mirror the entries' layout).
+  walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
       tb, S + 1, entries, c_lo + wv * 64u, NW * 64u, c_hi,
-      [&](const uint32_t (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
-        uint8_t* gmask = smask + static_cast<uint64_t>(g) * C;
-        // straight-line over the U hashes (no per-hash branch), so the
-        // compiler can keep several hashes' LDS reads in flight; lanes without
-        // an entry probe a harmless in-slice address and store nothing
-        uint32_t acc[U];
+      [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
+        uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
+        uint32_t ans[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-          uint32_t x = hv[u];
-          const uint32_t base = x & ((R - 1u) << 9);  // line offset * 512 stacked bytes (probe_entry)
-          const uint32_t delta = x >> 17;            // low 9 bits of rotr(h, 17)
-          acc[u] = 0xffu;
-          if constexpr (K > 0) {
+          const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+          uint32_t a = 0;
 #pragma unroll
-            for (int q = 0; q < K; q++) {
-              acc[u] &= sl[base | (x & 511u)];
-              x += delta;
+          for (int j = 0; j < 4; j++) {
+            uint32_t x = e4[j];
+            const uint32_t base = x & ((R - 1u) << 9);  // line offset * 512 stacked bytes (probe_entry)
+            const uint32_t delta = x >> 17;            // low 9 bits of rotr(h, 17)
+            uint32_t acc = 0xffu;
+            if constexpr (K > 0) {
+#pragma unroll
+              for (int q = 0; q < K; q++) {
+#if DLSM_ABL_NOLDS  // ablation (timing only, wrong answers): no LDS probe reads
+                acc &= (base | (x & 511u)) >> 3;
+#else
+                acc &= sl[base | (x & 511u)];
+#endif
+                x += delta;
+              }
+            } else {
+              for (int q = 0; q < k; q++) {
+                acc &= sl[base | (x & 511u)];
+                x += delta;
+              }
             }
-          } else {
-            for (int q = 0; q < k; q++) {
-              acc[u] &= sl[base | (x & 511u)];
-              x += delta;
-            }
+            a |= acc << (8 * j);
           }
+          ans[u] = a;
         }
 #pragma unroll
         for (int u = 0; u < U; u++)
-          if (ok[u]) gmask[idx[u]] = static_cast<uint8_t>(acc[u]);
+#if DLSM_ABL_NOSTORE  // ablation (timing only): almost no answer stores
+          if (ok[u] && ans[u] == 0x12345678u && (hv[u].x & 0xfff) == 0x123u) gmask[idx[u]] = ans[u];
+#else
+          if (ok[u]) gmask[idx[u]] = ans[u];
+#endif
       });
 }
 
@@ -945,15 +1008,16 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
                                                                  const uint16_t* __restrict__ pos,
                                                                  const uint8_t* __restrict__ smask,
                                                                  uint8_t* __restrict__ mask) {
-  __shared__ __attribute__((aligned(16))) uint8_t sm[C];
+  constexpr uint32_t CR = probe_region(C);
+  __shared__ __attribute__((aligned(16))) uint8_t sm[CR];
   const int tid = threadIdx.x;
   const uint64_t first = static_cast<uint64_t>(blockIdx.x) * C;
   const uint64_t left = n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
-  const uint32_t nvec = nk / 16u;
-  const uint4* s4 = reinterpret_cast<const uint4*>(smask + first);
+  // the chunk's answer region (bucket padding included; positions point into it)
+  const uint32_t nvec = (min(CR, nk + 4u * kMaxSlices) + 15u) / 16u;
+  const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(blockIdx.x) * CR);
   for (uint32_t v = tid; v < nvec; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
-  for (uint32_t b = nvec * 16u + tid; b < nk; b += kBlock) sm[b] = smask[first + b];
   __syncthreads();
   for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
     if (i0 + 8u <= nk) {
@@ -1253,11 +1317,12 @@ static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t 
                                   uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
                                   const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stacked);
+  constexpr int NT = DLSM_PROBE_NT;
   if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
-    probe_slice_kernel<LGR, 6, 1024, C><<<n_slices * parts, 1024, 0, s>>>(
+    probe_slice_kernel<LGR, 6, NT, C><<<n_slices * parts, NT, 0, s>>>(
         st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
   else
-    probe_slice_kernel<LGR, 0, 1024, C><<<n_slices * parts, 1024, 0, s>>>(
+    probe_slice_kernel<LGR, 0, NT, C><<<n_slices * parts, NT, 0, s>>>(
         st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
