@@ -257,6 +257,38 @@ __device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
 // `tile` is LDS scratch of K20Tile<NT, KPT>::kVec uint4 (K20 only).
 constexpr int kTileKPT = 2;  // keys per thread per LDS tile (20 KiB tiles at 512 threads)
 
+// K20 with tiles 0 and 1 already in pre[0] / pre[1]: two key tiles stay in
+// flight throughout -- while tile q is hashed, tile q+2 loads; while the last
+// two tiles are hashed, the NEXT chunk's tiles 0 and 1 load (persistent loop:
+// HBM reads continue through the bucket / scan / scatter / store phases).
+template <int NT, int PER>
+__device__ __forceinline__ void hash_chunk_k20_pipe(const KeyDesc& kd, uint64_t first, uint32_t nk,
+                                                    uint64_t next_first, uint32_t next_nk,
+                                                    uint4* tile, uint32_t (&h)[PER],
+                                                    uint4 (&pre)[2][K20Tile<NT, kTileKPT>::kPer]) {
+  const int t = threadIdx.x;
+  constexpr int KPT = kTileKPT;
+  using TL = K20Tile<NT, KPT>;
+  constexpr int NTILES = PER / KPT;
+  static_assert(NTILES >= 2, "two tiles in flight");
+  const uint8_t* base = kd.bytes + first * 20u;
+  const uint8_t* nbase = kd.bytes + next_first * 20u;
+#pragma unroll
+  for (int q = 0; q < NTILES; q++) {
+    k20_tile_store<NT, KPT>(tile, pre[q & 1]);
+    __syncthreads();
+    if (q + 2 < NTILES) {
+      if ((q + 2) * TL::kKeys < static_cast<int>(nk)) k20_tile_fetch<NT, KPT>(base, nk * 20u, q + 2, pre[q & 1]);
+    } else if (next_nk > static_cast<uint32_t>((q + 2 - NTILES) * TL::kKeys)) {
+      k20_tile_fetch<NT, KPT>(nbase, next_nk * 20u, q + 2 - NTILES, pre[q & 1]);
+    }
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
+#pragma unroll
+    for (int j = 0; j < KPT; j++) h[q * KPT + j] = hash_k20_lds(w + 5 * (j * NT + t));
+    __syncthreads();
+  }
+}
+
 template <int MODE, int NT, int PER>
 __device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, uint32_t nk,
                                            uint4* tile, uint32_t (&h)[PER]) {
@@ -861,14 +893,37 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
   __shared__ uint32_t wsum[NT / 64];
   const int tid = threadIdx.x;
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
+  auto chunk_keys = [&](uint32_t cc) {
+    const uint64_t left = kd.n - static_cast<uint64_t>(cc) * C;
+    return left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
+  };
+  // K20 (chunks of <= 8 keys per thread: more spills): the key tiles are
+  // software-pipelined across chunks (hash_chunk_k20_pipe) -- one resident
+  // workgroup per CU would otherwise leave its CU's HBM stream idle during
+  // the bucket / scan / scatter / store phases.
+  constexpr bool kPipe = MODE == KM_K20 && PER <= 8 && PER / kTileKPT >= 2;
+  uint4 pre[2][K20Tile<NT, kTileKPT>::kPer];
+  if constexpr (kPipe) {
+    if (blockIdx.x < nC) {
+      const uint8_t* b0 = kd.bytes + static_cast<uint64_t>(blockIdx.x) * C * 20u;
+      const uint32_t n0 = chunk_keys(blockIdx.x);
+      k20_tile_fetch<NT, kTileKPT>(b0, n0 * 20u, 0, pre[0]);
+      if (n0 > static_cast<uint32_t>(K20Tile<NT, kTileKPT>::kKeys)) k20_tile_fetch<NT, kTileKPT>(b0, n0 * 20u, 1, pre[1]);
+    }
+  }
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
   for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
     const uint64_t first = static_cast<uint64_t>(c) * C;
-    const uint64_t left = kd.n - first;
-    const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+    const uint32_t nk = chunk_keys(c);
     for (uint32_t b = tid; b <= S; b += NT) hist[b] = 0;
     uint32_t h[PER];
-    hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);  // ends with a barrier
+    if constexpr (kPipe) {
+      const uint32_t cn = c + gridDim.x;
+      hash_chunk_k20_pipe<NT, PER>(kd, first, nk, static_cast<uint64_t>(cn) * C, cn < nC ? chunk_keys(cn) : 0u,
+                                   tile, h, pre);  // ends with a barrier
+    } else {
+      hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);  // ends with a barrier
+    }
 #pragma unroll
     for (int r = 0; r < PER; r++) {
       const uint32_t i = r * NT + tid;
