@@ -541,18 +541,32 @@ __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowle
 
 // Copy n u32 / u16 staged in LDS to global memory with 16-byte stores (the
 // global base is 16-byte aligned: chunk starts are multiples of 4096 elements).
-template <int NT>
+// NTS: non-temporal 16-byte stores.  The probe's intermediates (≈520 MB per
+// 100 M keys) cannot stay in the 256 MiB Infinity Cache anyway, so streaming
+// them past it keeps it for the key stream (probe: −5 %); the build's 4 B/key
+// hashes do fit and are re-read by the slice pass, so the build keeps plain
+// stores.
+template <bool NTS>
+__device__ __forceinline__ void store16(uint4* g, const uint4& v) {
+  if constexpr (NTS) {
+    u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(g));
+  } else {
+    *g = v;
+  }
+}
+template <int NT, bool NTS = false>
 __device__ __forceinline__ void store_chunk_u32(uint32_t* g, const uint32_t* lds, uint32_t n) {
   const uint32_t nv = n / 4u;
   for (uint32_t v = threadIdx.x; v < nv; v += NT)
-    reinterpret_cast<uint4*>(g)[v] = reinterpret_cast<const uint4*>(lds)[v];
+    store16<NTS>(reinterpret_cast<uint4*>(g) + v, reinterpret_cast<const uint4*>(lds)[v]);
   for (uint32_t i = nv * 4u + threadIdx.x; i < n; i += NT) g[i] = lds[i];
 }
-template <int NT>
+template <int NT, bool NTS = false>
 __device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds, uint32_t n) {
   const uint32_t nv = n / 8u;
   for (uint32_t v = threadIdx.x; v < nv; v += NT)
-    reinterpret_cast<uint4*>(g)[v] = reinterpret_cast<const uint4*>(lds)[v];
+    store16<NTS>(reinterpret_cast<uint4*>(g) + v, reinterpret_cast<const uint4*>(lds)[v]);
   for (uint32_t i = nv * 8u + threadIdx.x; i < n; i += NT) g[i] = lds[i];
 }
 
@@ -963,8 +977,8 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
     }
     __syncthreads();
     // coalesced 16-byte stores of the bucketed entries and of the positions
-    store_chunk_u32<NT>(entries + static_cast<uint64_t>(c) * CR, stage, total);
-    store_chunk_u16<NT>(pos + first, rk, nk);
+    store_chunk_u32<NT, true>(entries + static_cast<uint64_t>(c) * CR, stage, total);
+    store_chunk_u16<NT, true>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
   }
 }
