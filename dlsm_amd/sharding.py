@@ -39,6 +39,8 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
         return value
     import torch
 
+    if dist.get_backend() != "nccl":
+        device = "cpu"  # gloo reduces host tensors
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
