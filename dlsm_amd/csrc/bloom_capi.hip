@@ -92,7 +92,7 @@ struct dlsm_ctx {
   int build_groups = 1;     // job groups of a build (1 = one partition + one slice launch)
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14)
-  int probe_lgr = 7;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
+  int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets

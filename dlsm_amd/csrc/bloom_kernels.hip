@@ -676,7 +676,11 @@ constexpr int kWalkU = 8;               // hashes in flight per lane (build segm
 #ifndef DLSM_PROBE_MINWAVES
 #define DLSM_PROBE_MINWAVES 1
 #endif
-constexpr int kProbeWalkU = DLSM_PROBE_U;  // probe walk: windows (hashes per lane) in flight
+#ifndef DLSM_PROBE_U8
+#define DLSM_PROBE_U8 2
+#endif
+constexpr int kProbeWalkU = DLSM_PROBE_U;    // probe walk, 64 KiB slices: unit windows in flight per wave
+constexpr int kProbeWalkU8 = DLSM_PROBE_U8;  // probe walk, 128 KiB slices
 
 template <int LGR>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
@@ -993,7 +997,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
-  constexpr int U = kProbeWalkU;
+  // window units in flight per wave: one 128 KiB slice per CU (LGR 8) leaves
+  // 4 waves per SIMD, so each carries two windows (measured best per shape)
+  constexpr int U = LGR >= 8 ? kProbeWalkU8 : kProbeWalkU;
   constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
   const int tid = threadIdx.x;

@@ -131,7 +131,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *   DLSM_OPT_PROBE_CHUNK_LG   log2 keys per probe partition chunk, 12..14 (default 13,
  *                             or $DLSM_PROBE_CHUNK_LG)
  *   DLSM_OPT_PROBE_SLICE_LG   log2 stacked filter lines per probe LDS slice, 7 (64 KiB)
- *                             or 8 (128 KiB) (default 7, or $DLSM_PROBE_SLICE_LG) */
+ *                             or 8 (128 KiB) (default 8, or $DLSM_PROBE_SLICE_LG) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
