@@ -74,7 +74,10 @@ struct LegacyJobDev {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
-constexpr int kBuildChunk = 4096;   // keys per partition chunk (build)
+#ifndef DLSM_BUILD_CHUNK
+#define DLSM_BUILD_CHUNK 4096
+#endif
+constexpr int kBuildChunk = DLSM_BUILD_CHUNK;  // keys per partition chunk (build)
 constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
 // u32 entries (and answer bytes) per probe chunk region: C keys plus up to 3
 // padding entries per slice bucket (buckets are padded to 16-byte units).

@@ -575,7 +575,7 @@ __device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds
 // partition).  One 512-thread workgroup per chunk of kBuildChunk keys of one
 // job.
 // ---------------------------------------------------------------------------
-constexpr int kPartBlock = 512;
+constexpr int kPartBlock = kBuildChunk / 8;  // 8 keys per thread (512 threads at 4,096-key chunks)
 
 template <int MODE, bool PART>
 __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
