@@ -324,10 +324,12 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
     oracle.full_probe(h_filters, h_q[: n1 * 20], n1, nthreads=1)
     s2 = time.perf_counter()
     L = lens.cpu().numpy()
-    parity = all(outs[s][: int(L[s])].cpu().numpy().tobytes() == built[s] for s in range(T))
-    parity = parity and bool(np.array_equal(mask[:nq].cpu().numpy(), cmask))
+    gpu_filters = [outs[s][: int(L[s])].cpu().numpy().tobytes() for s in range(T)]
+    gpu_mask = mask[:nq].cpu().numpy()
+    parity = all(gpu_filters[s] == built[s] for s in range(T))
+    parity = parity and bool(np.array_equal(gpu_mask, cmask))
     sample_keys = T * N + nq
-    return {
+    port = {
         "value": round(sample_keys / (t2 - t0) / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
         "kind": "port",
         "sample": f"build {T}x{N} keys ({threads} threads, one table per thread) + probe {nq} "
@@ -338,6 +340,24 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
                           "probe_mkeys_s": round(n1 / (s2 - s1) / 1e6, 2)},
         "host_cpu": cpu_model(),
         "gpu_output_matches_oracle": bool(parity),
+    }
+    # the reference's own bloom code (oracle/_ref/libref.so, built in place from
+    # /root/reference by build()) on the same sample, when it travelled with the tree
+    ref = oracle.ref_timed_baseline(h_tabs, N, h_filters, h_q, nq, bpk, threads)
+    if ref is None:
+        return port
+    rb, rp, rbuilt, rmask = ref
+    return {
+        "value": round(sample_keys / (rb + rp) / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
+        "kind": "reference",
+        "sample": port["sample"] + "; util/bloom_impl.h AddHash / HashMayMatch + util/hash.cc "
+                  "compiled from the reference (full_filter_block.cc's bookkeeping restated)",
+        "build_mkeys_s": round(T * N / rb / 1e6, 2),
+        "probe_mkeys_s": round(nq / rp / 1e6, 2),
+        "host_cpu": cpu_model(),
+        "gpu_output_matches_reference": bool(all(gpu_filters[s] == rbuilt[s] for s in range(T))
+                                             and np.array_equal(gpu_mask, rmask)),
+        "port": port,
     }
 
 

@@ -93,6 +93,47 @@ def lib():
     return _LIB
 
 
+def ref_timed_baseline(tables, n: int, filters: list, q: np.ndarray, nq: int, bpk: int,
+                       threads: int):
+    """Time the reference's own code (oracle/_ref/libref.so: util/bloom_impl.h
+    AddHash / HashMayMatch, util/hash.cc) on the host: one table per thread
+    for the build, lookups split over threads x every filter for the probe
+    (per-filter re-hash, as FullFilterBlockReader::KeyMayMatch does).  Returns
+    (build_s, probe_s, built filters, mask) or None without libref.so."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    R = ref_lib()
+    if R is None:
+        return None
+    offs = np.arange(n + 1, dtype=np.uint64) * 20
+    cap = full_filter_bytes(n, bpk)[0] + 64
+
+    def build_one(t):
+        out = np.zeros(cap, dtype=np.uint8)
+        ln = R.ref_full_build(t.ctypes.data_as(C.c_char_p), _ptr(offs, u64p), n, bpk, out.ctypes.data, cap)
+        return out[:ln].tobytes()
+
+    fa = [np.frombuffer(f, dtype=np.uint8) for f in filters]
+    fp = (C.c_void_p * len(fa))(*[a.ctypes.data for a in fa])
+    fl = np.array([a.size for a in fa], dtype=np.uint64)
+    mask = np.zeros(max(nq, 1), dtype=np.uint8)
+
+    def probe_part(r):
+        lo, hi = nq * r // threads, nq * (r + 1) // threads
+        if hi > lo:
+            R.ref_full_probe_many(fp, _ptr(fl, u64p), len(fa), q[lo * 20:].ctypes.data_as(C.c_char_p),
+                                  hi - lo, 20, mask[lo:].ctypes.data)
+
+    with ThreadPoolExecutor(max_workers=threads) as ex:  # ctypes calls release the GIL
+        t0 = time.perf_counter()
+        built = list(ex.map(build_one, tables))
+        t1 = time.perf_counter()
+        list(ex.map(probe_part, range(threads)))
+        t2 = time.perf_counter()
+    return t1 - t0, t2 - t1, built, mask[:nq]
+
+
 def ref_lib():
     """The reference compiled in place, or None (GPU box / reference absent)."""
     global _REF
@@ -112,6 +153,9 @@ def ref_lib():
         R.ref_full_build.restype = C.c_int64
         R.ref_full_build.argtypes = [cp, u64p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
         R.ref_full_may_match.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
+        R.ref_full_probe_many.restype = None
+        R.ref_full_probe_many.argtypes = [C.POINTER(C.c_void_p), u64p, C.c_int, cp, C.c_uint64,
+                                          C.c_uint32, C.c_void_p]
         R.ref_crc32c_extend.restype = C.c_uint32
         R.ref_crc32c_extend.argtypes = [C.c_uint32, cp, C.c_size_t]
         R.ref_crc32c_mask.restype = C.c_uint32

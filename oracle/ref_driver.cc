@@ -111,6 +111,19 @@ int ref_full_may_match(const char* key, size_t klen, const char* filter, size_t 
   return LegacyBloom::HashMayMatchPrepared(h, k, filter + off, 6) ? 1 : 0;
 }
 
+// Batch form of the reference reader (the reference has no MultiGet): for key
+// i and filter f, ref_full_may_match -- BloomHash recomputed per filter, as
+// every FullFilterBlockReader::KeyMayMatch call does.  mask[i] bit f.
+void ref_full_probe_many(const char* const* filters, const uint64_t* flens, int F, const char* keys,
+                         uint64_t n, uint32_t stride, uint8_t* mask) {
+  for (uint64_t i = 0; i < n; i++) {
+    uint8_t m = 0;
+    for (int f = 0; f < F; f++)
+      m |= static_cast<uint8_t>(ref_full_may_match(keys + i * stride, stride, filters[f], flens[f]) << f);
+    mask[i] = m;
+  }
+}
+
 uint32_t ref_crc32c_extend(uint32_t init, const char* data, size_t n) {
   return TimberSaw::crc32c::Extend(init, data, n);
 }
