@@ -176,13 +176,29 @@ bool is_k20(const dlsm_keyset& k) {
 }
 
 // Slice width for the sliced build: the smallest 2^lgR (lgR in [9, 11]) that
-// keeps every job at <= kMaxSlices slices.  Returns -1 if none fits.
+// keeps every job at <= kMaxSlices slices, then narrower (down to 2^7 lines,
+// 8 KiB) while the batch has fewer than two slice workgroups per CU -- a
+// batch of dLSM-sized flush tables (153,846 keys, 3,005 lines) would
+// otherwise leave most CUs idle.  Returns -1 if none fits.
 int choose_build_lgR(const std::vector<uint32_t>& Ls) {
-  for (int lg = 9; lg <= 11; lg++) {
+  auto slices = [&](int lg, uint64_t* total) {
     bool ok = true;
-    for (uint32_t L : Ls)
-      if (((static_cast<uint64_t>(L) + (1u << lg) - 1) >> lg) > kMaxSlices) ok = false;
-    if (ok) return lg;
+    *total = 0;
+    for (uint32_t L : Ls) {
+      const uint64_t n = (static_cast<uint64_t>(L) + (1u << lg) - 1) >> lg;
+      ok = ok && n <= kMaxSlices;
+      *total += std::max<uint64_t>(n, 1);
+    }
+    return ok;
+  };
+  uint64_t total = 0, t2 = 0;
+  for (int lg = 9; lg <= 11; lg++) {
+    if (!slices(lg, &total)) continue;
+    while (lg > 7 && total < 2u * kBuildSliceCUs && slices(lg - 1, &t2)) {
+      lg--;
+      total = t2;
+    }
+    return lg;
   }
   return -1;
 }
@@ -966,7 +982,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     else kr.bytes = kd.bytes + r0 * kd.key_len;
     // (slice, part) workgroups: about one resident wave of workgroups (256
     // CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at least one
-    // 64-chunk group per wave.
+    // chunk per wave (a part's waves split its chunks into equal groups).
     // ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU: a tuning knob
     // for the pipelined rounds, where a partition workgroup shares each CU)
     static const uint32_t per_cu_env = [] {
@@ -975,7 +991,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     }();
     const uint32_t resident = 256u * (per_cu_env ? per_cu_env : (lgR == 7 ? 2u : 1u));
     int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
-    parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 1024)));
+    parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 16)));
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
     DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ent, pos, tab, mode, lgC, ps));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));

@@ -74,6 +74,7 @@ struct LegacyJobDev {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
+constexpr uint32_t kBuildSliceCUs = 256;  // MI355X CUs: the build's slice-count target (choose_build_lgR)
 #ifndef DLSM_BUILD_CHUNK
 #define DLSM_BUILD_CHUNK 4096
 #endif

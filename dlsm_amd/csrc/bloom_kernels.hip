@@ -427,7 +427,9 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 }
 
 // One wave's walk over a slice's segments in the chunk groups g = g_first,
-// g_first + g_step, ... < g_end (64 chunks per group; chunk-major table rows of
+// g_first + g_step, ... < g_end (gs <= 64 chunks per group, one per lane: a
+// caller with few chunks per wave shrinks gs so every wave of the workgroup
+// gets a group instead of wave 0 walking them all; chunk-major table rows of
 // `rowlen` u16 bucket offsets, `tb` already offset to the slice's column).
 // Software-pipelined: window set i+1's hash loads (and the next group's table
 // rows, one group ahead) are issued before window set i is consumed, so every
@@ -443,6 +445,7 @@ struct SegWalk {
   const uint16_t* tb;
   const uint32_t* entries;
   uint32_t rowlen, g_step, g_end;
+  uint32_t gs;        // chunks per group (<= 64; lanes >= gs hold empty segments)
   uint32_t g;         // current group (first chunk)
   uint32_t e0;        // next window start in the current group
   uint32_t excl, dv, T;
@@ -461,7 +464,7 @@ struct SegWalk {
   __device__ __forceinline__ void setup(uint32_t row) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t a0 = (row & 0xffffu) / kPerE, a1 = (row >> 16) / kPerE;
-    const uint32_t cnt = g + lane < g_end ? a1 - a0 : 0u;
+    const uint32_t cnt = lane < gs && g + lane < g_end ? a1 - a0 : 0u;
     const uint32_t incl = wave_incl_scan_dpp(cnt);
     excl = incl - cnt;
     T = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
@@ -510,9 +513,10 @@ struct WinSet {
 
 template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, typename Act>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
-                                              uint32_t g_first, uint32_t g_step, uint32_t g_end, Act act) {
+                                              uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
+                                              Act act) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
-  SegWalk<U, CHUNK, E> w{tb, entries, rowlen, g_step, g_end};
+  SegWalk<U, CHUNK, E> w{tb, entries, rowlen, g_step, g_end, gs};
   if (!w.start(g_first)) return;
   WinSet<U, CHUNK, E> A, B;
   if (!w.next(A.idx, A.ok, A.g)) return;
@@ -717,8 +721,12 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       const uint16_t* tb = tab + J.tab0 + s;  // chunk-major rows of n_slices+1 u16
       const uint32_t* ent = entries + J.entry0;
       const int k = J.k;
+      // chunks per wave group: every wave gets a share of a small job's chunks
+      // (a job of >= 256 chunks keeps whole 64-chunk groups: measured 2 %
+      // faster at 391 chunks than 8 groups of 49, gpurun_out v19b)
+      const uint32_t gs = nC >= 256u ? 64u : max(1u, (nC + NW - 1) / NW);
       walk_segments<U, kBuildChunk>(
-          tb, J.n_slices + 1, ent, wv * 64u, NW * 64u, nC,
+          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
           [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
 #pragma unroll
             for (int u = 0; u < U; u++)
@@ -1030,8 +1038,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
+  const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
   walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
-      tb, S + 1, entries, c_lo + wv * 64u, NW * 64u, c_hi,
+      tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs,
       [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
         uint32_t ans[U];
@@ -1303,6 +1312,14 @@ hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, i
                               const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s) {
   if (n_slices == 0) return hipSuccess;
   switch (lgR) {
+    case 7:
+      full_slice_kernel<7><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
+                                                            slice_first);
+      break;
+    case 8:
+      full_slice_kernel<8><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
+                                                            slice_first);
+      break;
     case 9:
       full_slice_kernel<9><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
                                                             slice_first);
