@@ -181,6 +181,17 @@ __device__ __forceinline__ void lds_add_hash(uint32_t* line, uint32_t h, int k) 
   }
 }
 
+template <int K>
+__device__ __forceinline__ void lds_add_hash_k(uint32_t* line, uint32_t h) {
+  const uint32_t delta = bloom_delta(h);
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    const uint32_t bp = h & 511u;
+    atomicOr(&line[bp >> 5], 1u << (bp & 31u));
+    h += delta;
+  }
+}
+
 // Filter trailer (full_filter_block.cc:133-135): k byte + Fixed32 num_lines.
 __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
   uint8_t* t = out + static_cast<uint64_t>(L) * 64u;
@@ -728,9 +739,15 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       walk_segments<U, kBuildChunk>(
           tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
           [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
+            if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
 #pragma unroll
-            for (int u = 0; u < U; u++)
-              if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], k);
+              for (int u = 0; u < U; u++)
+                if (ok[u]) lds_add_hash_k<6>(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < U; u++)
+                if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], k);
+            }
           });
     } else {
       // Duplicates lowered the line count below the speculative one: the
