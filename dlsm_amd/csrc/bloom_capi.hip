@@ -175,6 +175,13 @@ bool is_k20(const dlsm_keyset& k) {
          (k.n == 0 || aligned(k.bytes, 16));
 }
 
+// 28-byte internal keys (20-byte user key + 8-byte trailer) straight from the
+// memtable / compaction iterators take the LDS-tiled K28 partition loaders.
+bool is_k28(const dlsm_keyset& k) {
+  return k.offsets == nullptr && k.key_len == 28 && k.suffix_len == 8 &&
+         (k.n == 0 || aligned(k.bytes, 16));
+}
+
 // Slice width for the sliced build: the smallest 2^lgR (lgR in [9, 11]) that
 // keeps every job at <= kMaxSlices slices, then narrower (down to 2^7 lines,
 // 8 KiB) while the batch has fewer than two slice workgroups per CU -- a
@@ -456,7 +463,7 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   DeviceGuard g(ctx->device);
   const int k = full_num_probes(bits_per_key);
   std::vector<uint32_t> Ls(n_jobs);
-  bool all_k20 = true, sliced_ok = ctx->path != 1;
+  bool all_k20 = true, all_k28 = true, sliced_ok = ctx->path != 1;
   for (int j = 0; j < n_jobs; j++) {
     const dlsm_build_job& b = jobs[j];
     DLSM_CHECK(validate_keyset(b.keys));
@@ -464,11 +471,12 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     if (b.keys.n > 0xffffffffull * kBuildChunk) return DLSM_E_ARG;
     Ls[j] = full_num_lines(b.keys.n, bits_per_key, nullptr);
     all_k20 = all_k20 && is_k20(b.keys);
+    all_k28 = all_k28 && is_k28(b.keys);
   }
   int lgR = choose_build_lgR(Ls);
   if (lgR < 0) sliced_ok = false;
   if (ctx->path == 2 && !sliced_ok) return DLSM_E_ARG;
-  const int mode = all_k20 ? KM_K20 : KM_GENERIC;
+  const int mode = all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC);
 
   std::vector<FullJobDev> hj(n_jobs);
   std::vector<uint32_t> starts(2 * n_jobs);
@@ -926,7 +934,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   if (!mask_dev) return DLSM_E_ARG;
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
-  const int mode = is_k20(*keys) ? KM_K20 : KM_GENERIC;
+  const int mode = is_k20(*keys) ? KM_K20 : (is_k28(*keys) ? KM_K28 : KM_GENERIC);
   const KeyDesc kd = to_desc(*keys);
   // Slices of 2^lgR stacked lines; a table with more than kMaxSlices slices
   // of 64 KiB moves to 128 KiB slices (one workgroup per CU).

@@ -12,7 +12,10 @@ namespace dlsm {
 // Key-load modes: K20 = fixed 20-byte keys at a 16-byte-aligned base (the
 // BASELINE shape; staged through LDS with 16-byte loads), GENERIC = any fixed
 // length / alignment or offsets (per-thread aligned-dword loads).
-enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1 };
+// K20: packed 20-B user keys; K28: packed 28-B internal keys hashed as
+// ExtractUserKey (suffix 8) -- both 16-B-aligned fixed stride, LDS-tiled in
+// the partition passes (other kernels take the K28 keys on the generic path)
+enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1, KM_K28 = 2 };
 
 struct KeyDesc {
   const uint8_t* bytes;

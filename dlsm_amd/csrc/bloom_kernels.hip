@@ -77,6 +77,8 @@ template <int MODE>
 __device__ __forceinline__ uint32_t key_hash(const KeyDesc& kd, uint64_t i) {
   if constexpr (MODE == KM_K20) {
     return hash_k20(kd.bytes + i * 20u);
+  } else if constexpr (MODE == KM_K28) {
+    return hash_k20(kd.bytes + i * 28u);  // ExtractUserKey: the first 20 of 28 bytes
   } else {
     uint64_t s, l;
     if (kd.offsets) {
@@ -211,17 +213,17 @@ __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int NT, int KPT>
+template <int NT, int KPT, int KB = 20>
 struct K20Tile {
   static constexpr int kKeys = KPT * NT;                 // keys per tile
-  static constexpr int kVec = kKeys * 20 / 16;           // uint4 per tile
+  static constexpr int kVec = kKeys * KB / 16;           // uint4 per tile
   static constexpr int kPer = (kVec + NT - 1) / NT;      // uint4 per thread
 };
 
-template <int NT, int KPT>
+template <int NT, int KPT, int KB = 20>
 __device__ __forceinline__ void k20_tile_fetch(const uint8_t* base, uint32_t nbytes, int q,
-                                               uint4 (&r)[K20Tile<NT, KPT>::kPer]) {
-  using TL = K20Tile<NT, KPT>;
+                                               uint4 (&r)[K20Tile<NT, KPT, KB>::kPer]) {
+  using TL = K20Tile<NT, KPT, KB>;
   const uint4* b4 = reinterpret_cast<const uint4*>(base) + q * TL::kVec;
   const uint32_t tile_off = q * TL::kVec * 16u;
 #pragma unroll
@@ -243,9 +245,9 @@ __device__ __forceinline__ void k20_tile_fetch(const uint8_t* base, uint32_t nby
   }
 }
 
-template <int NT, int KPT>
-__device__ __forceinline__ void k20_tile_store(uint4* lds, const uint4 (&r)[K20Tile<NT, KPT>::kPer]) {
-  using TL = K20Tile<NT, KPT>;
+template <int NT, int KPT, int KB = 20>
+__device__ __forceinline__ void k20_tile_store(uint4* lds, const uint4 (&r)[K20Tile<NT, KPT, KB>::kPer]) {
+  using TL = K20Tile<NT, KPT, KB>;
 #pragma unroll
   for (int v = 0; v < TL::kPer; v++) {
     const uint32_t u = v * NT + threadIdx.x;
@@ -267,35 +269,44 @@ __device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
 // Hash keys [first, first+nk) of kd into h[PER] (key r*NT+t -> thread t, h[r]).
 // `tile` is LDS scratch of K20Tile<NT, KPT>::kVec uint4 (K20 only).
 constexpr int kTileKPT = 2;  // keys per thread per LDS tile (20 KiB tiles at 512 threads)
+// K28 (28-byte internal keys, ExtractUserKey = the first 20 bytes): the same
+// LDS tiles at stride 7 dwords (odd: conflict-free), one key per thread per
+// tile so a 1024-thread tile stays at 28 KiB (two persistent probe
+// partition workgroups per CU).  The 8-byte trailers ride along in the
+// coalesced 16-byte loads and are never hashed.
+template <int MODE>
+constexpr int mode_kb() { return MODE == KM_K28 ? 28 : 20; }
+template <int KB>
+constexpr int tile_kpt() { return KB == 20 ? kTileKPT : 1; }
 
 // K20 with tiles 0 and 1 already in pre[0] / pre[1]: two key tiles stay in
 // flight throughout -- while tile q is hashed, tile q+2 loads; while the last
 // two tiles are hashed, the NEXT chunk's tiles 0 and 1 load (persistent loop:
 // HBM reads continue through the bucket / scan / scatter / store phases).
-template <int NT, int PER>
+template <int NT, int PER, int KB = 20>
 __device__ __forceinline__ void hash_chunk_k20_pipe(const KeyDesc& kd, uint64_t first, uint32_t nk,
                                                     uint64_t next_first, uint32_t next_nk,
                                                     uint4* tile, uint32_t (&h)[PER],
-                                                    uint4 (&pre)[2][K20Tile<NT, kTileKPT>::kPer]) {
+                                                    uint4 (&pre)[2][K20Tile<NT, tile_kpt<KB>(), KB>::kPer]) {
   const int t = threadIdx.x;
-  constexpr int KPT = kTileKPT;
-  using TL = K20Tile<NT, KPT>;
+  constexpr int KPT = tile_kpt<KB>();
+  using TL = K20Tile<NT, KPT, KB>;
   constexpr int NTILES = PER / KPT;
   static_assert(NTILES >= 2, "two tiles in flight");
-  const uint8_t* base = kd.bytes + first * 20u;
-  const uint8_t* nbase = kd.bytes + next_first * 20u;
+  const uint8_t* base = kd.bytes + first * KB;
+  const uint8_t* nbase = kd.bytes + next_first * KB;
 #pragma unroll
   for (int q = 0; q < NTILES; q++) {
-    k20_tile_store<NT, KPT>(tile, pre[q & 1]);
+    k20_tile_store<NT, KPT, KB>(tile, pre[q & 1]);
     __syncthreads();
     if (q + 2 < NTILES) {
-      if ((q + 2) * TL::kKeys < static_cast<int>(nk)) k20_tile_fetch<NT, KPT>(base, nk * 20u, q + 2, pre[q & 1]);
+      if ((q + 2) * TL::kKeys < static_cast<int>(nk)) k20_tile_fetch<NT, KPT, KB>(base, nk * KB, q + 2, pre[q & 1]);
     } else if (next_nk > static_cast<uint32_t>((q + 2 - NTILES) * TL::kKeys)) {
-      k20_tile_fetch<NT, KPT>(nbase, next_nk * 20u, q + 2 - NTILES, pre[q & 1]);
+      k20_tile_fetch<NT, KPT, KB>(nbase, next_nk * KB, q + 2 - NTILES, pre[q & 1]);
     }
     const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
 #pragma unroll
-    for (int j = 0; j < KPT; j++) h[q * KPT + j] = hash_k20_lds(w + 5 * (j * NT + t));
+    for (int j = 0; j < KPT; j++) h[q * KPT + j] = hash_k20_lds(w + (KB / 4) * (j * NT + t));
     __syncthreads();
   }
 }
@@ -304,25 +315,26 @@ template <int MODE, int NT, int PER>
 __device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, uint32_t nk,
                                            uint4* tile, uint32_t (&h)[PER]) {
   const int t = threadIdx.x;
-  if constexpr (MODE == KM_K20) {
-    constexpr int KPT = kTileKPT;
-    using TL = K20Tile<NT, KPT>;
+  if constexpr (MODE == KM_K20 || MODE == KM_K28) {
+    constexpr int KB = mode_kb<MODE>();
+    constexpr int KPT = tile_kpt<KB>();
+    using TL = K20Tile<NT, KPT, KB>;
     constexpr int NTILES = PER / KPT;
-    const uint8_t* base = kd.bytes + first * 20u;
-    const uint32_t nbytes = nk * 20u;
+    const uint8_t* base = kd.bytes + first * KB;
+    const uint32_t nbytes = nk * KB;
     uint4 pre[TL::kPer];
-    k20_tile_fetch<NT, KPT>(base, nbytes, 0, pre);
+    k20_tile_fetch<NT, KPT, KB>(base, nbytes, 0, pre);
 #pragma unroll
     for (int q = 0; q < NTILES; q++) {
-      k20_tile_store<NT, KPT>(tile, pre);
+      k20_tile_store<NT, KPT, KB>(tile, pre);
       __syncthreads();
       if (q + 1 < NTILES && (q + 1) * TL::kKeys < static_cast<int>(nk))
-        k20_tile_fetch<NT, KPT>(base, nbytes, q + 1, pre);
+        k20_tile_fetch<NT, KPT, KB>(base, nbytes, q + 1, pre);
       const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
 #pragma unroll
       for (int j = 0; j < KPT; j++) {
         const int r = q * KPT + j;
-        h[r] = hash_k20_lds(w + 5 * (j * NT + t));
+        h[r] = hash_k20_lds(w + (KB / 4) * (j * NT + t));
       }
       __syncthreads();
     }
@@ -600,8 +612,10 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   constexpr int C = kBuildChunk;
   constexpr int PER = C / kPartBlock;
   // key tile (K20), then the staging area of the bucketed hashes (both modes)
-  __shared__ __attribute__((aligned(16))) uint4 tile[K20Tile<kPartBlock, kTileKPT>::kVec];
-  static_assert(K20Tile<kPartBlock, kTileKPT>::kVec * 16 >= C * 4, "staging fits the tile");
+  constexpr int KB = mode_kb<MODE>();
+  constexpr int TKV = K20Tile<kPartBlock, tile_kpt<KB>(), KB>::kVec;
+  constexpr int TVB = TKV > C / 4 ? TKV : C / 4;  // the staging area needs C u32
+  __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
   __shared__ uint32_t wsum[kPartBlock / 64];
@@ -619,7 +633,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   uint32_t h[PER];
   hash_chunk<MODE, kPartBlock, PER>(J.keys, first, nk, tile, h);
   uint32_t prev0 = ~h[0];
-  if (first > 0) prev0 = key_hash<MODE == KM_K20 ? KM_K20 : KM_GENERIC>(J.keys, first - 1);
+  if (first > 0) prev0 = key_hash<MODE>(J.keys, first - 1);
   const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, __shfl(prev0, 0, 64), lastw, wsum);
   if (tid == 0) dchunk[bid] = cnt;
   if constexpr (!PART) return;
@@ -925,9 +939,11 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
   constexpr int PER = C / NT;
   constexpr uint32_t CR = probe_region(C);
   // the key tile doubles as the bucketed-entry staging area (CR u32)
-  constexpr int TV = K20Tile<NT, kTileKPT>::kVec > static_cast<int>(CR / 4) ? K20Tile<NT, kTileKPT>::kVec
-                                                                           : static_cast<int>(CR / 4);
-  static_assert(PER % kTileKPT == 0 && CR <= 65536, "chunk shape");
+  constexpr int KB = mode_kb<MODE>();
+  constexpr int KPT = tile_kpt<KB>();
+  using TL = K20Tile<NT, KPT, KB>;
+  constexpr int TV = TL::kVec > static_cast<int>(CR / 4) ? TL::kVec : static_cast<int>(CR / 4);
+  static_assert(PER % KPT == 0 && CR <= 65536, "chunk shape");
   __shared__ __attribute__((aligned(16))) uint4 tile[TV];
   __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
   __shared__ uint8_t sb[C];                                // slice (S <= 256)
@@ -944,14 +960,14 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
   // software-pipelined across chunks (hash_chunk_k20_pipe) -- one resident
   // workgroup per CU would otherwise leave its CU's HBM stream idle during
   // the bucket / scan / scatter / store phases.
-  constexpr bool kPipe = MODE == KM_K20 && PER <= 8 && PER / kTileKPT >= 2;
-  uint4 pre[2][K20Tile<NT, kTileKPT>::kPer];
+  constexpr bool kPipe = MODE != KM_GENERIC && PER <= 8 && PER / KPT >= 2;
+  uint4 pre[2][TL::kPer];
   if constexpr (kPipe) {
     if (blockIdx.x < nC) {
-      const uint8_t* b0 = kd.bytes + static_cast<uint64_t>(blockIdx.x) * C * 20u;
+      const uint8_t* b0 = kd.bytes + static_cast<uint64_t>(blockIdx.x) * C * KB;
       const uint32_t n0 = chunk_keys(blockIdx.x);
-      k20_tile_fetch<NT, kTileKPT>(b0, n0 * 20u, 0, pre[0]);
-      if (n0 > static_cast<uint32_t>(K20Tile<NT, kTileKPT>::kKeys)) k20_tile_fetch<NT, kTileKPT>(b0, n0 * 20u, 1, pre[1]);
+      k20_tile_fetch<NT, KPT, KB>(b0, n0 * KB, 0, pre[0]);
+      if (n0 > static_cast<uint32_t>(TL::kKeys)) k20_tile_fetch<NT, KPT, KB>(b0, n0 * KB, 1, pre[1]);
     }
   }
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
@@ -962,7 +978,7 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
     uint32_t h[PER];
     if constexpr (kPipe) {
       const uint32_t cn = c + gridDim.x;
-      hash_chunk_k20_pipe<NT, PER>(kd, first, nk, static_cast<uint64_t>(cn) * C, cn < nC ? chunk_keys(cn) : 0u,
+      hash_chunk_k20_pipe<NT, PER, KB>(kd, first, nk, static_cast<uint64_t>(cn) * C, cn < nC ? chunk_keys(cn) : 0u,
                                    tile, h, pre);  // ends with a barrier
     } else {
       hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);  // ends with a barrier
@@ -1288,6 +1304,9 @@ hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, in
   if (mode == KM_K20)
     full_partition_kernel<KM_K20, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                           nullptr, nullptr, 0, 0u);
+  else if (mode == KM_K28)
+    full_partition_kernel<KM_K28, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
+                                                                          nullptr, nullptr, 0, 0u);
   else
     full_partition_kernel<KM_GENERIC, false><<<total_chunks, kPartBlock, 0, s>>>(
         jobs, chunk0s, n_jobs, dchunk, nullptr, nullptr, 0, 0u);
@@ -1317,6 +1336,9 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
   if (n_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
     full_partition_kernel<KM_K20, true><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
+                                                                     entries, tab, lgR, chunk_first);
+  else if (mode == KM_K28)
+    full_partition_kernel<KM_K28, true><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                      entries, tab, lgR, chunk_first);
   else
     full_partition_kernel<KM_GENERIC, true><<<n_chunks, kPartBlock, 0, s>>>(
@@ -1403,6 +1425,9 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
   const uint32_t g = per_cu ? std::min(nC, per_cu * device_cus()) : nC;
   if (mode == KM_K20)
     probe_partition_kernel<KM_K20, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+                                                          entries, pos, tab);
+  else if (mode == KM_K28)
+    probe_partition_kernel<KM_K28, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                           entries, pos, tab);
   else
     probe_partition_kernel<KM_GENERIC, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,

@@ -203,3 +203,53 @@ def test_gpu_rejects_fixed_keys_shorter_than_suffix(gpu):
 
     with pytest.raises(dlsm_amd.DlsmError):
         gpu.full_build([dlsm_amd.Keys(np.zeros(64, np.uint8), 4, 4, suffix_len=8)], 10)
+
+
+def _internal28(user20: np.ndarray, n: int, seed: int) -> np.ndarray:
+    """Packed 28-byte internal keys: each 20-byte user key + an 8-byte trailer
+    (random seq/type bytes: the trailer must never reach the hash)."""
+    trl = np.random.default_rng(seed).integers(0, 256, size=(n, 8), dtype=np.uint8)
+    return np.ascontiguousarray(np.hstack([user20.reshape(n, 20), trl]).reshape(-1))
+
+
+@pytest.mark.gpu
+def test_gpu_k28_tiled_build_and_probe(gpu):
+    """Fixed-stride 28-byte internal keys (suffix_len 8) take the LDS-tiled K28
+    partition loaders in the build and the sliced probe: filters and 8-filter
+    masks must equal the oracle's over the stripped 20-byte user keys.  Sizes
+    cross the build's 4,096-key and the probe's 8,192-key chunk boundaries
+    with ragged tails; device (torch) and host (staged) buffers both go in."""
+    import torch
+
+    import dlsm_amd
+
+    sizes = [1, 4095, 4097, 8193, 100_003, 153_846]
+    users = [oracle.dbbench_keys(s, 7, n) for s, n in enumerate(sizes)]
+    ints = [_internal28(u, n, 10 + s) for s, (u, n) in enumerate(zip(users, sizes))]
+    want = [oracle.full_build(u, n) for u, n in zip(users, sizes)]
+    got = gpu.full_build([dlsm_amd.Keys(d, n, 28, suffix_len=8) for d, n in zip(ints, sizes)], 10)
+    assert got == want
+    dev = [torch.from_numpy(d).cuda() for d in ints]
+    outs = [torch.zeros(len(w) + 64, dtype=torch.uint8, device="cuda") for w in want]
+    lens = torch.zeros(len(sizes), dtype=torch.uint64, device="cuda")
+    gpu.full_build_dev([dlsm_amd.Keys(d, n, 28, suffix_len=8) for d, n in zip(dev, sizes)], outs, lens, 10)
+    gpu.sync()
+    for o, w, ln in zip(outs, want, lens.cpu().tolist()):
+        assert ln == len(w) and bytes(o[:ln].cpu().numpy()) == w
+
+    # 8 stacked filters of one line count (sliced probe), ~50 % absent lookups
+    nf = 60_000
+    fkeys = [oracle.dbbench_keys(f, 8, nf) for f in range(8)]
+    filters = [oracle.full_build(k, nf) for k in fkeys]
+    nq = 8192 * 9 + 1234
+    qu = oracle.keys_from_values(oracle.mt_values(7, 16 * nf, nq))
+    want_mask = oracle.full_probe(filters, qu, nq, nthreads=4)
+    fs = gpu.filterset(filters)
+    q28 = _internal28(qu, nq, 99)
+    assert np.array_equal(gpu.full_probe(fs, dlsm_amd.Keys(q28, nq, 28, suffix_len=8)), want_mask)
+    mask = torch.zeros(nq, dtype=torch.uint8, device="cuda")
+    gpu.full_probe_dev(fs, dlsm_amd.Keys(torch.from_numpy(q28).cuda(), nq, 28, suffix_len=8), mask)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy(), want_mask)
+    assert 0.2 < (want_mask != 0).mean() < 0.8
+    fs.close()
