@@ -268,6 +268,9 @@ __device__ __forceinline__ uint32_t hash_k20_lds(const uint32_t* w) {
 
 // Hash keys [first, first+nk) of kd into h[PER] (key r*NT+t -> thread t, h[r]).
 // `tile` is LDS scratch of K20Tile<NT, KPT>::kVec uint4 (K20 only).
+#ifndef DLSM_TILE_ALL
+#define DLSM_TILE_ALL 1  // hash_chunk: all key tiles of a chunk loaded at once (when they fit 16 uint4)
+#endif
 constexpr int kTileKPT = 2;  // keys per thread per LDS tile (20 KiB tiles at 512 threads)
 // K28 (28-byte internal keys, ExtractUserKey = the first 20 bytes): the same
 // LDS tiles at stride 7 dwords (odd: conflict-free), one key per thread per
@@ -322,6 +325,24 @@ __device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, ui
     constexpr int NTILES = PER / KPT;
     const uint8_t* base = kd.bytes + first * KB;
     const uint32_t nbytes = nk * KB;
+    if constexpr (DLSM_TILE_ALL && NTILES * TL::kPer <= 16) {
+      // every tile's loads in flight at once (one HBM round trip per chunk,
+      // not one per tile: short, non-persistent grids are latency-bound)
+      uint4 all[NTILES][TL::kPer];
+#pragma unroll
+      for (int q = 0; q < NTILES; q++)
+        if (q == 0 || q * TL::kKeys < static_cast<int>(nk)) k20_tile_fetch<NT, KPT, KB>(base, nbytes, q, all[q]);
+#pragma unroll
+      for (int q = 0; q < NTILES; q++) {
+        k20_tile_store<NT, KPT, KB>(tile, all[q]);
+        __syncthreads();
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
+#pragma unroll
+        for (int j = 0; j < KPT; j++) h[q * KPT + j] = hash_k20_lds(w + (KB / 4) * (j * NT + t));
+        __syncthreads();
+      }
+      return;
+    }
     uint4 pre[TL::kPer];
     k20_tile_fetch<NT, KPT, KB>(base, nbytes, 0, pre);
 #pragma unroll
