@@ -651,11 +651,14 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   const uint64_t left = J.keys.n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
 
+  // the key before the chunk (AddKey's dedup neighbour), hashed before the
+  // chunk's tile loads so its round trip overlaps them
+  uint32_t prev_h = 0;
+  if (first > 0 && tid == 0) prev_h = key_hash<MODE>(J.keys, first - 1);  // only wave 0 lane 0 reads it
   uint32_t h[PER];
   hash_chunk<MODE, kPartBlock, PER>(J.keys, first, nk, tile, h);
-  uint32_t prev0 = ~h[0];
-  if (first > 0) prev0 = key_hash<MODE>(J.keys, first - 1);
-  const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, __shfl(prev0, 0, 64), lastw, wsum);
+  const uint32_t prev0 = first > 0 ? __shfl(prev_h, 0, 64) : ~__shfl(h[0], 0, 64);
+  const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, prev0, lastw, wsum);
   if (tid == 0) dchunk[bid] = cnt;
   if constexpr (!PART) return;
 
