@@ -46,8 +46,8 @@ def cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--keys-per-table", type=int, default=1_600_000)
     ap.add_argument("--tables", type=int, default=16)
     ap.add_argument("--lookups", type=int, default=100_000_000)
