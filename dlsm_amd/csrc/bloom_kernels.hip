@@ -956,21 +956,29 @@ __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
 // grouped by slice, every bucket padded to a multiple of 4 entries with
 // kProbePadEntry, so the slice pass moves whole 16-byte units; pos[i] = where
 // key i went.  NT threads per chunk of C keys (C/NT keys per thread).
-template <int MODE, int NT, int C>
+template <int MODE, int NT, int C, int H = 1>
 __global__ __launch_bounds__(NT) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
-  constexpr int PER = C / NT;
+  // H > 1: the chunk is hashed and bucketed in H units of CH keys (the tile
+  // pipeline's unit stays CH), ranks keep counting across units, so every
+  // bucket of the C-key chunk is one contiguous run: C-key chunks (longer
+  // runs for the slice pass's gather) at the register cost of CH-key ones.
+  // Entries of all but the last unit wait in LDS (`park`) until the chunk's
+  // bucket offsets are known.
+  constexpr int CH = C / H;
+  constexpr int PER = CH / NT;
   constexpr uint32_t CR = probe_region(C);
   // the key tile doubles as the bucketed-entry staging area (CR u32)
   constexpr int KB = mode_kb<MODE>();
   constexpr int KPT = tile_kpt<KB>();
   using TL = K20Tile<NT, KPT, KB>;
   constexpr int TV = TL::kVec > static_cast<int>(CR / 4) ? TL::kVec : static_cast<int>(CR / 4);
-  static_assert(PER % KPT == 0 && CR <= 65536, "chunk shape");
+  static_assert(PER % KPT == 0 && CR <= 65536 && C % H == 0, "chunk shape");
   __shared__ __attribute__((aligned(16))) uint4 tile[TV];
   __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
   __shared__ uint8_t sb[C];                                // slice (S <= 256)
+  __shared__ uint32_t park[H > 1 ? (H - 1) * CH : 1];      // entries of units 0..H-2
   __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint8_t npad[kMaxSlices + 1];
   __shared__ uint32_t wsum[NT / 64];
@@ -980,16 +988,20 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
     const uint64_t left = kd.n - static_cast<uint64_t>(cc) * C;
     return left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
   };
-  // K20 (chunks of <= 8 keys per thread: more spills): the key tiles are
-  // software-pipelined across chunks (hash_chunk_k20_pipe) -- one resident
-  // workgroup per CU would otherwise leave its CU's HBM stream idle during
-  // the bucket / scan / scatter / store phases.
+  auto unit_keys = [&](uint32_t nk, int u) {  // keys of unit u of a chunk of nk keys
+    const uint32_t b = static_cast<uint32_t>(u) * CH;
+    return nk > b ? min(nk - b, static_cast<uint32_t>(CH)) : 0u;
+  };
+  // K20 / K28 (units of <= 8 keys per thread: more spills): the key tiles are
+  // software-pipelined across units and chunks (hash_chunk_k20_pipe) -- one
+  // resident workgroup per CU would otherwise leave its CU's HBM stream idle
+  // during the bucket / scan / scatter / store phases.
   constexpr bool kPipe = MODE != KM_GENERIC && PER <= 8 && PER / KPT >= 2;
   uint4 pre[2][TL::kPer];
   if constexpr (kPipe) {
     if (blockIdx.x < nC) {
       const uint8_t* b0 = kd.bytes + static_cast<uint64_t>(blockIdx.x) * C * KB;
-      const uint32_t n0 = chunk_keys(blockIdx.x);
+      const uint32_t n0 = unit_keys(chunk_keys(blockIdx.x), 0);
       k20_tile_fetch<NT, KPT, KB>(b0, n0 * KB, 0, pre[0]);
       if (n0 > static_cast<uint32_t>(TL::kKeys)) k20_tile_fetch<NT, KPT, KB>(b0, n0 * KB, 1, pre[1]);
     }
@@ -1000,22 +1012,30 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
     const uint32_t nk = chunk_keys(c);
     for (uint32_t b = tid; b <= S; b += NT) hist[b] = 0;
     uint32_t h[PER];
-    if constexpr (kPipe) {
-      const uint32_t cn = c + gridDim.x;
-      hash_chunk_k20_pipe<NT, PER, KB>(kd, first, nk, static_cast<uint64_t>(cn) * C, cn < nC ? chunk_keys(cn) : 0u,
-                                   tile, h, pre);  // ends with a barrier
-    } else {
-      hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);  // ends with a barrier
-    }
 #pragma unroll
-    for (int r = 0; r < PER; r++) {
-      const uint32_t i = r * NT + tid;
-      if (i < nk) {
-        const uint32_t line = fastmod(h[r], L, magic);
-        const uint32_t sl = line >> lgR;
-        sb[i] = static_cast<uint8_t>(sl);
-        rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
-        h[r] = probe_entry(h[r], line & ((1u << lgR) - 1u));
+    for (int u = 0; u < H; u++) {
+      const uint32_t nku = unit_keys(nk, u);
+      const uint64_t fu = first + static_cast<uint64_t>(u) * CH;
+      if constexpr (kPipe) {
+        const uint32_t cn = c + gridDim.x;
+        const uint64_t nf = u + 1 < H ? fu + CH : static_cast<uint64_t>(cn) * C;
+        const uint32_t nn = u + 1 < H ? unit_keys(nk, u + 1) : (cn < nC ? unit_keys(chunk_keys(cn), 0) : 0u);
+        hash_chunk_k20_pipe<NT, PER, KB>(kd, fu, nku, nf, nn, tile, h, pre);  // ends with a barrier
+      } else {
+        hash_chunk<MODE, NT, PER>(kd, fu, nku, tile, h);  // ends with a barrier
+      }
+#pragma unroll
+      for (int r = 0; r < PER; r++) {
+        const uint32_t il = r * NT + tid;
+        const uint32_t i = static_cast<uint32_t>(u) * CH + il;
+        if (il < nku) {
+          const uint32_t line = fastmod(h[r], L, magic);
+          const uint32_t sl = line >> lgR;
+          sb[i] = static_cast<uint8_t>(sl);
+          rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+          h[r] = probe_entry(h[r], line & ((1u << lgR) - 1u));
+          if (u + 1 < H) park[i] = h[r];
+        }
       }
     }
     __syncthreads();
@@ -1035,12 +1055,22 @@ __global__ __launch_bounds__(NT) void probe_partition_kernel(
       if (np > 1) stage[end - 2] = kProbePadEntry;
       if (np > 2) stage[end - 3] = kProbePadEntry;
     }
+    const uint32_t nkl = unit_keys(nk, H - 1);
 #pragma unroll
-    for (int r = 0; r < PER; r++) {
-      const uint32_t i = r * NT + tid;
-      if (i < nk) {
+    for (int r = 0; r < PER; r++) {  // the last unit, from registers
+      const uint32_t il = r * NT + tid;
+      const uint32_t i = static_cast<uint32_t>(H - 1) * CH + il;
+      if (il < nkl) {
         const uint32_t p = hist[sb[i]] + rk[i];
         stage[p] = h[r];
+        rk[i] = static_cast<uint16_t>(p);
+      }
+    }
+    if constexpr (H > 1) {  // the parked units
+      const uint32_t np = min(nk, static_cast<uint32_t>((H - 1) * CH));
+      for (uint32_t i = tid; i < np; i += NT) {
+        const uint32_t p = hist[sb[i]] + rk[i];
+        stage[p] = park[i];
         rk[i] = static_cast<uint16_t>(p);
       }
     }
@@ -1432,9 +1462,12 @@ static uint32_t device_cus() {
   return cus[dev];
 }
 
+#ifndef DLSM_PROBE_UNITS14
+#define DLSM_PROBE_UNITS14 2
+#endif
 // Probe chunk shapes: C keys per partition workgroup of NT threads.
 //   lgC 12: C = 4096, 512 threads;  13: 8192, 1024;  14: 16384, 1024.
-template <int C, int NT>
+template <int C, int NT, int H = 1>
 static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                      uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                      uint16_t* tab, int mode, hipStream_t s) {
@@ -1448,13 +1481,13 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
   }();
   const uint32_t g = per_cu ? std::min(nC, per_cu * device_cus()) : nC;
   if (mode == KM_K20)
-    probe_partition_kernel<KM_K20, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K20, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                           entries, pos, tab);
   else if (mode == KM_K28)
-    probe_partition_kernel<KM_K28, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K28, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                           entries, pos, tab);
   else
-    probe_partition_kernel<KM_GENERIC, NT, C><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_GENERIC, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                               entries, pos, tab);
   return hipGetLastError();
 }
@@ -1465,7 +1498,8 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
   switch (lgC) {
     case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
     case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
-    case 14: return probe_partition_as<16384, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    // 16,384-key chunks bucketed as two 8,192-key units (DLSM_PROBE_UNITS14)
+    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
     default: return hipErrorInvalidValue;
   }
 }
