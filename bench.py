@@ -57,8 +57,8 @@ def main():
     ap.add_argument("--probe-round", type=int, default=None,
                     help="keys per pipelined probe round (0 = one round, the default)")
     ap.add_argument("--build-groups", type=int, default=0, help="pipelined build job groups (0/1 = one group)")
-    ap.add_argument("--probe-chunk-lg", type=int, default=14,
-                    help="log2 keys per probe partition chunk (12..14; library default 14)")
+    ap.add_argument("--probe-chunk-lg", type=int, default=13,
+                    help="log2 keys per probe partition chunk (12..14; library default 13)")
     ap.add_argument("--probe-slice-lg", type=int, default=8,
                     help="log2 stacked lines per probe LDS slice (7, 8; library default 8)")
     ap.add_argument("--traffic", default=os.path.join(os.path.dirname(os.path.abspath(__file__)),

@@ -91,7 +91,7 @@ struct dlsm_ctx {
   int path = 0;
   int build_groups = 1;     // job groups of a build (1 = one partition + one slice launch)
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
-  int probe_lgc = 14;        // log2 keys per probe partition chunk (12..14; 14 = two 8,192-key units)
+  int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14; 13 = two 4,096-key units, 512 threads)
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   // build workspace
   DevBuf<uint32_t> entries;

@@ -957,7 +957,7 @@ __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
 // kProbePadEntry, so the slice pass moves whole 16-byte units; pos[i] = where
 // key i went.  NT threads per chunk of C keys (C/NT keys per thread).
 template <int MODE, int NT, int C, int H = 1>
-__global__ __launch_bounds__(NT) void probe_partition_kernel(
+__global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
   // H > 1: the chunk is hashed and bucketed in H units of CH keys (the tile
@@ -1462,6 +1462,9 @@ static uint32_t device_cus() {
   return cus[dev];
 }
 
+#ifndef DLSM_PROBE_P13_HALF
+#define DLSM_PROBE_P13_HALF 1
+#endif
 #ifndef DLSM_PROBE_UNITS14
 #define DLSM_PROBE_UNITS14 2
 #endif
@@ -1497,7 +1500,12 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
                                   uint16_t* tab, int mode, int lgC, hipStream_t s) {
   switch (lgC) {
     case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+#if DLSM_PROBE_P13_HALF
+    // 512-thread workgroups of two 4,096-key units (two resident per CU)
+    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+#else
     case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+#endif
     // 16,384-key chunks bucketed as two 8,192-key units (DLSM_PROBE_UNITS14)
     case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
     default: return hipErrorInvalidValue;

@@ -128,7 +128,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *   DLSM_OPT_PROBE_ROUND_KEYS keys per pipelined probe round (default 0 = one
  *                             round, or $DLSM_PROBE_ROUND_KEYS)
  *   DLSM_OPT_BUILD_GROUPS     job groups of a pipelined build (0/1 = one, up to 4)
- *   DLSM_OPT_PROBE_CHUNK_LG   log2 keys per probe partition chunk, 12..14 (default 14,
+ *   DLSM_OPT_PROBE_CHUNK_LG   log2 keys per probe partition chunk, 12..14 (default 13,
  *                             or $DLSM_PROBE_CHUNK_LG)
  *   DLSM_OPT_PROBE_SLICE_LG   log2 stacked filter lines per probe LDS slice, 7 (64 KiB)
  *                             or 8 (128 KiB) (default 8, or $DLSM_PROBE_SLICE_LG) */

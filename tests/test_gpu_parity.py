@@ -262,7 +262,7 @@ def test_full_probe_shapes(gpu, orc, chunk_lg, slice_lg):
             gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
             gpu.sync()
         finally:
-            gpu.set_probe_shape(14, 8)
+            gpu.set_probe_shape(13, 8)
             gpu.set_path(0)
         fs.close()
         assert np.array_equal(mask.cpu().numpy(), want), (n_per, nq)
