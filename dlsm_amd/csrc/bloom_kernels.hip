@@ -623,6 +623,22 @@ __device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds
 // partition).  One 512-thread workgroup per chunk of kBuildChunk keys of one
 // job.
 // ---------------------------------------------------------------------------
+// Build entries (DLSM_BUILD_LINE_IN_ENTRY): AddHash reads only hash bits
+// [0, 9) and [17, 26) (bitpos = h & 511 stepping by rotr(h, 17), positions
+// mod 512, util/bloom_impl.h:427-443), so the partition parks the key's line
+// offset inside its slice (< 2^11) in bits [9, 17) and [26, 29): the slice
+// pass needs no modulo.  The full hash is gone, so the rare slice fallback
+// (duplicates lowered L) re-hashes the keys.
+__device__ __forceinline__ uint32_t build_entry(uint32_t h, uint32_t off) {
+  return (h & 0xE3FE01FFu) | ((off & 0xffu) << 9) | ((off >> 8) << 26);
+}
+__device__ __forceinline__ uint32_t build_entry_off(uint32_t e) {
+  return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
+}
+
+#ifndef DLSM_BUILD_LINE_IN_ENTRY
+#define DLSM_BUILD_LINE_IN_ENTRY 1
+#endif
 constexpr int kPartBlock = kBuildChunk / 8;  // 8 keys per thread (512 threads at 4,096-key chunks)
 
 template <int MODE, bool PART>
@@ -670,8 +686,12 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
-      const uint32_t s = fastmod(h[r], J.L_spec, J.magic_spec) >> lgR;
+      const uint32_t line = fastmod(h[r], J.L_spec, J.magic_spec);
+      const uint32_t s = line >> lgR;
       code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
+#if DLSM_BUILD_LINE_IN_ENTRY
+      h[r] = build_entry(h[r], line & ((1u << lgR) - 1u));
+#endif
     }
   }
   __syncthreads();
@@ -777,6 +797,17 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       walk_segments<U, kBuildChunk>(
           tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
           [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
+#if DLSM_BUILD_LINE_IN_ENTRY
+            if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
+#pragma unroll
+              for (int u = 0; u < U; u++)
+                if (ok[u]) lds_add_hash_k<6>(sl + build_entry_off(hv[u]) * 16u, hv[u]);
+            } else {
+#pragma unroll
+              for (int u = 0; u < U; u++)
+                if (ok[u]) lds_add_hash(sl + build_entry_off(hv[u]) * 16u, hv[u], k);
+            }
+#else
             if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
 #pragma unroll
               for (int u = 0; u < U; u++)
@@ -786,13 +817,19 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
               for (int u = 0; u < U; u++)
                 if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], k);
             }
+#endif
           });
     } else {
       // Duplicates lowered the line count below the speculative one: the
       // partition used the wrong modulus, so scan every hash of the job.
+#if DLSM_BUILD_LINE_IN_ENTRY
+      for (uint64_t e = tid; e < J.keys.n; e += kSliceBlock) {
+        const uint32_t hv = key_hash<KM_GENERIC>(J.keys, e);
+#else
       const uint32_t* ent = entries + J.entry0;
       for (uint64_t e = tid; e < J.keys.n; e += kSliceBlock) {
         const uint32_t hv = ent[e];
+#endif
         const uint32_t line = fastmod(hv, L, magic);
         if ((line >> LGR) == s) lds_add_hash(sl + (line - lo_line) * 16u, hv, J.k);
       }
