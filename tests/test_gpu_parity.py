@@ -240,11 +240,14 @@ def test_full_probe_pipelined_rounds(gpu, orc, round_keys):
 
 @pytest.mark.parametrize("chunk_lg", [12, 13, 14])
 @pytest.mark.parametrize("slice_lg", [7, 8])
-def test_full_probe_shapes(gpu, orc, chunk_lg, slice_lg):
-    """Every sliced-probe shape (chunk of 4096/8192/16384 keys x 64/128 KiB
-    LDS slices) gives the oracle's masks: a ragged key count, filters whose
-    line count is not a multiple of the slice, and a 60-line filter set
-    (one partial slice)."""
+@pytest.mark.parametrize("key_len", [20, 28])
+def test_full_probe_shapes(gpu, orc, chunk_lg, slice_lg, key_len):
+    """Every sliced-probe shape (chunk of 4096/8192/16384 keys -- the latter
+    two bucketed in two units -- x 64/128 KiB LDS slices) gives the oracle's
+    masks, for 20-byte user keys (K20 tiles) and 28-byte internal keys
+    (suffix 8, K28 tiles): a ragged key count, filters whose line count is
+    not a multiple of the slice, and a 60-line filter set (one partial
+    slice)."""
     import torch
 
     import dlsm_amd
@@ -254,12 +257,15 @@ def test_full_probe_shapes(gpu, orc, chunk_lg, slice_lg):
         q = orc.keys_from_values(orc.mt_values(91 + chunk_lg, 8 * n_per * 2, nq))
         want = orc.full_probe(filters, q, nq, nthreads=8)
         fs = gpu.filterset(filters)
+        if key_len == 28:  # + an 8-byte trailer the hash must skip
+            trl = np.random.default_rng(chunk_lg).integers(0, 256, size=(nq, 8), dtype=np.uint8)
+            q = np.ascontiguousarray(np.hstack([q.reshape(nq, 20), trl]).reshape(-1))
         qd = torch.from_numpy(q).cuda()
         mask = torch.full((nq,), 0xEE, dtype=torch.uint8, device="cuda")
         gpu.set_path(2)
         gpu.set_probe_shape(chunk_lg, slice_lg)
         try:
-            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
+            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, key_len, suffix_len=key_len - 20), mask)
             gpu.sync()
         finally:
             gpu.set_probe_shape(13, 8)
