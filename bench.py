@@ -1,15 +1,19 @@
 """Headline benchmark: Bloom build+probe Mkeys/s (device-resident), 20 B keys,
 10 bits/key -- BASELINE.json's metric.
 
-One step (per GPU, weak scaling: SSTables shard one-per-GPU with no
-collective):
-  * build: 16 SSTable full filters (12 subcompaction + 4 flush outputs) of
-    1.6M db_bench keys each, in one device-resident batch call
-    (dlsm_bloom_full_build_dev) -- BASELINE configs[1]/[3] shape;
-  * probe: 100M 20-byte lookups (v = mt19937_64(1000+rank) mod 25.6M) against
-    8 stacked per-level full filters (dlsm_bloom_full_probe_dev) --
-    BASELINE configs[2].
-value = (build keys + probe keys) over all ranks / max-over-ranks wall time.
+One step = one pass of the path over one batch:
+  * build: the 16 SSTable full filters of one flush/compaction round (12
+    subcompaction + 4 flush outputs, 1.6 M db_bench keys each) in one
+    device-resident batch call (dlsm_bloom_full_build_dev) -- configs[1]/[3];
+  * probe: 100 M 20-byte lookups (v = mt19937_64(1000) mod 25.6 M) against 8
+    stacked per-level full filters (dlsm_bloom_full_probe_dev) -- configs[2].
+
+--gpus N > 1 (one process per GPU, torch.distributed.run) defaults to STRONG
+scaling, the north star's config 4: the SAME 16 SSTables split s mod N, the
+filter set built once and broadcast to every rank, the ONE 100 M-key lookup
+stream split into N contiguous shards (dlsm_amd/sharding.py).  --scaling weak
+gives every rank its own 16 tables and 100 M lookups instead.
+value = (build keys + probe keys) of the whole job / max-over-ranks wall time.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -65,7 +69,10 @@ def main():
                                                       "profiles", "traffic.json"),
                     help="PMC traffic summary (scripts/pmc_traffic.py) reported as roofline.traffic "
                          "when its config matches this run")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--scaling", choices=["auto", "strong", "weak"], default="auto",
+                    help="strong (default: one fixed job split over the ranks) or weak (a job per rank)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-cores CPU baseline (0 = every host core)")
     ap.add_argument("--cpu-probe-sample", type=int, default=10_000_000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -76,7 +83,6 @@ def main():
 
     import dlsm_amd
     from dlsm_amd import sharding as SH
-    from dlsm_amd import workload as W
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -95,6 +101,8 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # strong by default at every N (at N = 1 the two shapes are the same job)
+    scaling = args.scaling if args.scaling != "auto" else "strong"
 
     N, T, Q, F, bpk = args.keys_per_table, args.tables, args.lookups, args.filters, args.bits_per_key
     ctx = dlsm_amd.Context(local)
@@ -108,39 +116,15 @@ def main():
 
     # ---- inputs, resident in HBM before timing ---------------------------
     t_in = time.time()
-    with torch.cuda.stream(stream):
-        tables, outs = [], []
-        for s in range(T):
-            first, step = SH.table_values(rank, s, T, N)
-            v = torch.arange(N, device=dev, dtype=torch.int64) * step + first
-            tables.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), N, 20))
-            outs.append(torch.zeros(dlsm_amd.full_size(N, bpk)[0], dtype=torch.uint8, device=dev))
-        lens = torch.zeros(T, dtype=torch.uint64, device=dev)
-        # the F stacked per-level filters probed by the lookups: filter f <- v = F*i + f
-        ftabs, fouts = [], []
-        for f in range(F):
-            v = torch.arange(N, device=dev, dtype=torch.int64) * F + f
-            ftabs.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), N, 20))
-            fouts.append(torch.zeros(dlsm_amd.full_size(N, bpk)[0], dtype=torch.uint8, device=dev))
-        flens = torch.zeros(F, dtype=torch.uint64, device=dev)
-    ctx.full_build_dev(ftabs, fouts, flens, bpk)
-    ctx.sync()
-    fl = flens.cpu().numpy()
-    filters = [fouts[f][: int(fl[f])] for f in range(F)]
-    fs = ctx.filterset(filters, on_device=True)
-    qv = W.mt19937_64(SH.lookup_seed(rank), Q) % np.uint64(2 * F * N)
-    qkeys = W.dbbench_keys_torch(torch.from_numpy(qv.astype(np.int64)).to(dev))
-    qk = dlsm_amd.Keys(qkeys, Q, 20)
-    mask = torch.empty(Q * fs.mask_bytes, dtype=torch.uint8, device=dev)
+    work = SH.plan(rank, world, T, N, Q, scaling)
+    inp = SH.make_inputs(ctx, work, N, F, bpk, dev, stream=stream, dist=dist)
     torch.cuda.synchronize()
-    log(f"[rank {rank}] inputs ready in {time.time() - t_in:.1f}s")
-
-    def step():
-        ctx.full_build_dev(tables, outs, lens, bpk)
-        ctx.full_probe_dev(fs, qk, mask)
+    log(f"[rank {rank}] {scaling}: tables {work.tables}, lookups [{work.lookup_lo}, {work.lookup_hi}) "
+        f"ready in {time.time() - t_in:.1f}s")
+    tables, outs, lens, fs, qk, mask = inp.tables, inp.outs, inp.lens, inp.fs, inp.lookups, inp.mask
 
     for _ in range(args.warmup):
-        step()
+        SH.step(ctx, inp, bpk)
     ctx.sync()
 
     # ---- timed region ----------------------------------------------------
@@ -152,9 +136,11 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        ctx.full_build_dev(tables, outs, lens, bpk)
+        if tables:
+            ctx.full_build_dev(tables, outs, lens, bpk)
         evs[i][1].record(stream)
-        ctx.full_probe_dev(fs, qk, mask)
+        if qk.n:
+            ctx.full_probe_dev(fs, qk, mask)
         evs[i][2].record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
@@ -165,15 +151,26 @@ def main():
     build_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
     probe_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
 
-    keys_per_step = T * N + Q
-    value = keys_per_step * world * args.steps / elapsed / 1e6
-    filt_bytes = int(fl.sum())
-    probe_bytes = Q * (20 + fs.mask_bytes) + filt_bytes           # 21.16 B/key
-    build_bytes = T * N * 20 + int(lens.cpu().numpy().sum())       # 21.25 B/key
+    # keys of the whole job per step (every rank's share)
+    rank_keys = len(tables) * N + qk.n
+    job_keys = (T * N + Q) if scaling == "strong" else (T * N + Q) * world
+    value = job_keys * args.steps / elapsed / 1e6
+    filt_bytes = sum(int(f.numel()) for f in inp.filters)
+    nb = max(1, len(tables) * N)
+    probe_bytes = qk.n * (20 + fs.mask_bytes) + filt_bytes           # 21.16 B/key
+    build_bytes = len(tables) * N * 20 + int(lens.cpu().numpy()[: len(tables)].sum())  # 21.25 B/key
     probe_gbs = probe_bytes / (probe_ms * 1e-3) / 1e9
     build_gbs = build_bytes / (build_ms * 1e-3) / 1e9
     dominant = "probe" if probe_ms >= build_ms else "build"
     ach = probe_gbs if dominant == "probe" else build_gbs
+    if scaling == "strong":
+        par = f"strong: {T} SSTables split s mod {world}, filters replicated, {Q} lookups sharded x{world}"
+        wl = (f"build {T} SSTable full filters x {N} keys (one batch) + probe {Q} lookups vs {F} "
+              f"stacked filters, split over {world} GPU(s)")
+    else:
+        par = f"weak: sstable-sharded x{world}, no collective"
+        wl = (f"per GPU: build {T} SSTable full filters x {N} keys (one batch) + probe "
+              f"{Q} lookups vs {F} stacked filters")
 
     result = {
         "metric": "Bloom build+probe Mkeys/s (device-resident), 20B keys, 10 bits/key",
@@ -184,29 +181,30 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic db_bench keys (GenerateKeyFromInt), mt19937_64 lookups",
         "config": {
-            "workload": (f"per GPU: build {T} SSTable full filters x {N} keys (one batch) + probe "
-                         f"{Q} lookups vs {F} stacked filters"),
+            "workload": wl,
             "key_bytes": 20, "bits_per_key": bpk, "tables": T, "keys_per_table": N,
-            "lookups": Q, "filters": F, "parallelism": f"sstable-sharded x{world}, no collective",
+            "lookups": Q, "filters": F, "parallelism": par,
+            "rank0_tables": work.tables, "rank0_lookups": qk.n,
             "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
             "probe_round_keys": args.probe_round, "build_groups": args.build_groups,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {
-            "bound": "hbm", "kernel": f"{dominant} pass", "achieved": round(ach, 1),
+            "bound": "hbm", "kernel": f"{dominant} pass (rank 0's share)", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
         },
-        "build": {"ms": round(build_ms, 4), "mkeys_s": round(T * N / build_ms / 1e3, 1),
-                  "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / (T * N), 3)},
-        "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(Q / probe_ms / 1e3, 1),
-                  "alg_GBs": round(probe_gbs, 1), "alg_bytes_per_key": round(probe_bytes / Q, 3)},
+        "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
+                  "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
+        "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, qk.n) / probe_ms / 1e3, 1),
+                  "alg_GBs": round(probe_gbs, 1), "alg_bytes_per_key": round(probe_bytes / max(1, qk.n), 3)},
     }
+    del rank_keys
 
     traffic = load_traffic(args.traffic, result["config"], dominant)
     if traffic:
@@ -219,9 +217,13 @@ def main():
     # ---- host-inclusive (PCIe) rate, N=1 only: recorded, never `value` ----
     if world == 1 and not args.no_e2e:
         result["e2e"] = e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev)
+        # the same build with the job table changing every call (a flush
+        # stream hands over new tables each time: the upload is paid)
+        result["build"]["rotating_batches_ms"] = round(rotating_build_ms(ctx, stream, tables, outs, lens, bpk), 4)
 
-    # ---- CPU baseline (oracle restatement, host cores), rank 0 at N=1 ----
+    # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if world == 1 and rank == 0 and not args.no_cpu:
+        filters = [f for f in inp.filters]
         result["cpu_baseline"] = cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk)
 
     if rank == 0:
@@ -298,67 +300,91 @@ def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):
             "note": "H2D keys + build + probe + D2H filters/masks, pinned host buffers"}
 
 
+def host_cores() -> int:
+    """Host cores this process may use: the CPU affinity set, capped by a
+    cgroup CPU quota when one is set (a GPU box's share of its host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
-    """The oracle (clean-room C restatement with the reference's cost structure)
-    on the host cores, on a bounded sample; also cross-checks the GPU output."""
+    """The CPU path timed on this box's host cores on a bounded sample of the
+    bench workload, at T = 1 and T = all cores: the reference's own code
+    (oracle/_ref/libref.so, built in place from /root/reference, when it
+    travelled with the tree) else the oracle's C restatement -- `kind` says
+    which.  Also cross-checks the GPU output against it."""
     import numpy as np
 
     import oracle
 
     oracle.lib()
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    cores = host_cores()
+    threads = args.cpu_threads or cores
     h_tabs = [t.data.cpu().numpy() for t in tables]
     h_filters = [f.cpu().numpy().tobytes() for f in filters]
     nq = min(args.cpu_probe_sample, qk.n)
-    h_q = qk.data[: nq * 20].cpu().numpy()
-    t0 = time.perf_counter()
-    built = oracle.full_build_many(h_tabs, [N] * T, 20, bpk, threads)
-    t1 = time.perf_counter()
-    cmask = oracle.full_probe(h_filters, h_q, nq, nthreads=threads)
-    t2 = time.perf_counter()
-    # single-thread reference point on one table + 1M lookups
-    s0 = time.perf_counter()
-    oracle.full_build(h_tabs[0], N, bpk=bpk)
-    s1 = time.perf_counter()
     n1 = min(1_000_000, nq)
-    oracle.full_probe(h_filters, h_q[: n1 * 20], n1, nthreads=1)
-    s2 = time.perf_counter()
+    h_q = qk.data[: nq * 20].cpu().numpy()
     L = lens.cpu().numpy()
     gpu_filters = [outs[s][: int(L[s])].cpu().numpy().tobytes() for s in range(T)]
     gpu_mask = mask[:nq].cpu().numpy()
-    parity = all(gpu_filters[s] == built[s] for s in range(T))
-    parity = parity and bool(np.array_equal(gpu_mask, cmask))
+    kind = "reference" if oracle.ref_lib() is not None else "port"
+    one = oracle.timed_cpu_baseline(kind, h_tabs[:1], N, h_filters, h_q[: n1 * 20], n1, bpk, 1)
+    allc = oracle.timed_cpu_baseline(kind, h_tabs, N, h_filters, h_q, nq, bpk, threads)
+    parity = (all(gpu_filters[s] == allc["built"][s] for s in range(T))
+              and bool(np.array_equal(gpu_mask, allc["mask"])) and one["built"][0] == gpu_filters[0])
     sample_keys = T * N + nq
-    port = {
-        "value": round(sample_keys / (t2 - t0) / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
-        "kind": "port",
-        "sample": f"build {T}x{N} keys ({threads} threads, one table per thread) + probe {nq} "
-                  f"lookups x {len(filters)} filters (re-hash per filter)",
-        "build_mkeys_s": round(T * N / (t1 - t0) / 1e6, 2),
-        "probe_mkeys_s": round(nq / (t2 - t1) / 1e6, 2),
-        "single_thread": {"build_mkeys_s": round(N / (s1 - s0) / 1e6, 2),
-                          "probe_mkeys_s": round(n1 / (s2 - s1) / 1e6, 2)},
+
+    def rates(r, nt, nqq, nth):
+        return {"build_mkeys_s": round(nt * N / r["build_s"] / 1e6, 2),
+                "probe_mkeys_s": round(nqq / r["probe_s"] / 1e6, 2),
+                "legacy_create_mkeys_s": round(r["legacy_tables"] * N / r["legacy_s"] / 1e6, 2),
+                # one table per thread: a table's build time on one core
+                "build_ms_per_table": round(r["build_s"] * min(nth, nt) / nt * 1e3, 3)}
+
+    out = {
+        "value": round(sample_keys / (allc["build_s"] + allc["probe_s"]) / 1e6, 2), "unit": "Mkeys/s",
+        "cores": threads, "kind": kind,
+        "sample": (f"build {T}x{N} keys (one SSTable per thread, FullFilterBlockBuilder) + probe {nq} "
+                   f"lookups x {len(filters)} filters (lookups split over the threads, BloomHash per "
+                   f"filter like KeyMayMatch), on all {threads} host cores; T=1: 1 table + {n1} lookups"),
+        "all_cores": rates(allc, T, nq, threads),
+        "single_thread": rates(one, 1, n1, 1),
+        "legacy_note": "util/bloom.cc CreateFilter (legacy FilterPolicy format) over the same tables",
         "host_cpu": cpu_model(),
-        "gpu_output_matches_oracle": bool(parity),
+        "host_cores_available": cores,
+        "gpu_output_matches_" + kind: bool(parity),
     }
-    # the reference's own bloom code (oracle/_ref/libref.so, built in place from
-    # /root/reference by build()) on the same sample, when it travelled with the tree
-    ref = oracle.ref_timed_baseline(h_tabs, N, h_filters, h_q, nq, bpk, threads)
-    if ref is None:
-        return port
-    rb, rp, rbuilt, rmask = ref
-    return {
-        "value": round(sample_keys / (rb + rp) / 1e6, 2), "unit": "Mkeys/s", "cores": threads,
-        "kind": "reference",
-        "sample": port["sample"] + "; util/bloom_impl.h AddHash / HashMayMatch + util/hash.cc "
-                  "compiled from the reference (full_filter_block.cc's bookkeeping restated)",
-        "build_mkeys_s": round(T * N / rb / 1e6, 2),
-        "probe_mkeys_s": round(nq / rp / 1e6, 2),
-        "host_cpu": cpu_model(),
-        "gpu_output_matches_reference": bool(all(gpu_filters[s] == rbuilt[s] for s in range(T))
-                                             and np.array_equal(gpu_mask, rmask)),
-        "port": port,
-    }
+    if kind == "reference":
+        out["sample"] += ("; util/bloom_impl.h AddHash / HashMayMatch + util/hash.cc + util/bloom.cc "
+                          "compiled from the reference (full_filter_block.cc's bookkeeping restated)")
+    return out
+
+
+def rotating_build_ms(ctx, stream, tables, outs, lens, bpk, reps=10):
+    """Build ms when consecutive calls alternate between two different job
+    tables (output slots swapped): every call uploads its job table, as a
+    flush stream that hands over new tables each time does."""
+    import torch
+
+    if len(tables) < 2:
+        return float("nan")
+    outs_b = outs[1:] + outs[:1]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for r in range(reps):
+        ctx.full_build_dev(tables, outs if r % 2 == 0 else outs_b, lens, bpk)
+    e1.record(stream)
+    stream.synchronize()
+    ctx.full_build_dev(tables, outs, lens, bpk)  # leave the slots as the timed loop wrote them
+    ctx.sync()
+    return e0.elapsed_time(e1) / reps
 
 
 if __name__ == "__main__":

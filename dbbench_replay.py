@@ -1,6 +1,7 @@
 """db_bench-shape replay with the GPU filter path plugged in (BASELINE config 5,
 SURVEY.md §8d): `db_bench --benchmarks=fillrandom,readrandom --value_size=400
---bloom_bits=10 --threads=16`, host buffers in and out (H2D / D2H included).
+--bloom_bits=10 --threads=16 --num=N`, host buffers in and out (H2D / D2H
+included in every timed call).
 
 Real db_bench cannot run here or on the GPU box: Env::Default() builds an
 RDMA_Manager (util/env_posix.cc:36-42) that needs ibverbs, a memory node and
@@ -13,21 +14,34 @@ connection.conf.  This replays the part that reaches the filter path:
   deterministic stand-in for the reference's concurrent interleaving); every
   153,846 entries (db/memtable.h:7) the memtable flushes: its user keys sorted,
   one entry per user key (FlushJob::BuildTable, db/memtable_list.cc:855-886)
-  -> one full filter per flushed SSTable, built on the GPU from HOST keys into
+  -> a level-0 SSTable whose full filter is built on the GPU from HOST keys into
   HOST slots (dlsm_bloom_full_build: H2D keys + build + D2H filters).
+* leveled compaction with dLSM's constants, a model of DBImpl::
+  BackgroundCompaction / VersionSet::PickCompaction (db/version_set.cc:
+  1340-1400, 1816-1870): level 0 compacts as soon as it holds
+  kL0_CompactionTrigger = 1 file (db/dbformat.h:31); level L >= 1 when its bytes
+  exceed max_mega_bytes_for_level_base = 256 MiB x 10^(L-1) (db/dbformat.h:52,
+  version_set.cc:48-59), taking the next file after the level's compact
+  pointer; the inputs merge with the overlapping files of level L+1 into
+  outputs of at most max_file_size = 64 MiB (include/TimberSaw/options.h:157;
+  64 MiB / 436 B per entry = 153,846 entries), a single input with no overlap
+  moves down unchanged (Compaction::IsTrivialMove, version_set.cc:2112-2121).
+  Every compaction's outputs are ONE batched GPU filter build from host keys
+  (the outputs of one compaction round, built together).
 * readrandom (:1379-1404): thread t reads k = Random64(1000 + threads + t + 1)
-  .Next() % (num * threads); each Get visits the level-0 flush files newest
-  first (Version::ForEachOverlapping) and checks their filters -> one batched
-  dlsm_version_probe_dev per call from HOST keys (H2D keys + probe + D2H
-  masks).  No compaction is modelled: every flush stays in level 0 (at most 59
-  files -- pick --num accordingly).
+  .Next() % (num * threads); each Get visits the files Version::Get would
+  (level-0 newest first, then one file per level: ForEachOverlapping,
+  version_set.cc:273-321) and checks their filters -> one batched
+  dlsm_version_probe_dev per batch of host keys (H2D keys + probe + D2H masks).
 
-Prints one JSON line.  Parity of these calls against the oracle is covered by
-tests/ (test_dbbench_replay.py runs a small replay and checks it).
+Prints one JSON line.  Parity against the oracle: tests/test_dbbench_replay.py
+(every filter and Get of a small replay) and tests/replay_fullsize_check.py
+(sampled, at --num 6,250,000 x 16 threads = 100 M writes).
 """
 from __future__ import annotations
 
 import argparse
+import bisect
 import json
 import os
 import sys
@@ -41,7 +55,12 @@ sys.path.insert(0, ROOT)
 import dlsm_amd  # noqa: E402
 from dlsm_amd import workload as W  # noqa: E402
 
-MEMTABLE_ENTRIES = 153_846  # db/memtable.h:7
+MEMTABLE_ENTRIES = 153_846         # db/memtable.h:7
+ENTRY_BYTES = 436                  # 20 B key + 8 B seq/type + 400 B value + ~8 B framing
+MAX_FILE_ENTRIES = 153_846         # max_file_size 64 MiB (options.h:157) / ENTRY_BYTES
+L0_TRIGGER = 1                     # config::kL0_CompactionTrigger (db/dbformat.h:31)
+LEVEL_BASE_BYTES = 256 * 1048576   # config::max_mega_bytes_for_level_base (db/dbformat.h:52)
+NUM_LEVELS = 6                     # config::kNumLevels (db/dbformat.h:26)
 
 
 def fill_stream(num: int, threads: int) -> np.ndarray:
@@ -64,79 +83,205 @@ def flushes(stream: np.ndarray):
     return out
 
 
-def run(num: int, threads: int, bpk: int, device: int = 0, reps: int = 3):
+def max_bytes_for_level(level: int) -> float:
+    r = float(LEVEL_BASE_BYTES)
+    while level > 1:
+        r *= 10
+        level -= 1
+    return r
+
+
+class SSTable:
+    __slots__ = ("values", "number", "filter")
+
+    def __init__(self, values, number, filt):
+        self.values, self.number, self.filter = values, number, filt
+
+    @property
+    def smallest(self):
+        return int(self.values[0])
+
+    @property
+    def largest(self):
+        return int(self.values[-1])
+
+
+class LSM:
+    """Leveled LSM over key VALUES (the filter path needs only the user keys);
+    every new SSTable's filter is built on the GPU from host keys."""
+
+    def __init__(self, ctx, bpk: int, on_build=None):
+        self.ctx, self.bpk = ctx, bpk
+        self.levels = [[] for _ in range(NUM_LEVELS)]
+        self.pointer = [None] * NUM_LEVELS  # compact_index_: largest value last compacted
+        self.next_number = 1
+        self.on_build = on_build  # test hook: (values list, filters list)
+        self.stats = {"flush_builds": 0, "flush_keys": 0, "flush_s": 0.0,
+                      "compactions": 0, "trivial_moves": 0, "compaction_builds": 0,
+                      "compaction_keys": 0, "compaction_s": 0.0, "merge_s": 0.0}
+
+    def _build(self, value_sets, kind):
+        tables = [dlsm_amd.Keys(W.dbbench_keys_np(v), v.size, 20) for v in value_sets]
+        t0 = time.perf_counter()
+        filters = self.ctx.full_build(tables, self.bpk)  # host keys -> host slots
+        dt = time.perf_counter() - t0
+        self.stats[kind + "_builds"] += len(value_sets)
+        self.stats[kind + "_keys"] += int(sum(v.size for v in value_sets))
+        self.stats[kind + "_s"] += dt
+        if self.on_build:
+            self.on_build(value_sets, filters)
+        out = []
+        for v, f in zip(value_sets, filters):
+            out.append(SSTable(v, self.next_number, f))
+            self.next_number += 1
+        return out
+
+    def flush(self, values):
+        self.levels[0].extend(self._build([values], "flush"))
+        self.compact_while_needed()
+
+    def _score(self, level):
+        if level == 0:
+            return len(self.levels[0]) / L0_TRIGGER
+        return sum(f.values.size for f in self.levels[level]) * ENTRY_BYTES / max_bytes_for_level(level)
+
+    def compact_while_needed(self):
+        while True:
+            scores = [(self._score(lv), -lv) for lv in range(NUM_LEVELS - 1)]
+            best, neg = max(scores)
+            if best < 1:
+                return
+            self.compact(-neg)
+
+    def compact(self, level):
+        files = self.levels[level]
+        if level == 0:
+            inputs = list(files)  # level-0 files overlap: all of them (trigger 1: usually one)
+        else:
+            p = self.pointer[level]
+            cand = [f for f in files if p is None or f.largest > p]
+            inputs = [cand[0] if cand else files[0]]
+        lo = min(f.smallest for f in inputs)
+        hi = max(f.largest for f in inputs)
+        nxt = self.levels[level + 1]
+        over = [f for f in nxt if not (f.largest < lo or f.smallest > hi)]
+        self.pointer[level] = hi
+        self.stats["compactions"] += 1
+        if level > 0 and len(inputs) == 1 and not over:  # IsTrivialMove
+            files.remove(inputs[0])
+            self._insert(level + 1, [inputs[0]])
+            self.stats["trivial_moves"] += 1
+            return
+        t0 = time.perf_counter()
+        merged = np.concatenate([f.values for f in inputs + over])
+        merged.sort(kind="stable")  # sorted runs: timsort merges them
+        keep = np.empty(merged.size, dtype=bool)
+        keep[0] = True
+        np.not_equal(merged[1:], merged[:-1], out=keep[1:])
+        merged = merged[keep]
+        outs = [merged[s:s + MAX_FILE_ENTRIES] for s in range(0, merged.size, MAX_FILE_ENTRIES)]
+        self.stats["merge_s"] += time.perf_counter() - t0
+        new = self._build(outs, "compaction")
+        for f in inputs:
+            files.remove(f)
+        for f in over:
+            nxt.remove(f)
+        self._insert(level + 1, new)
+
+    def _insert(self, level, new):
+        lst = self.levels[level]
+        for f in new:  # levels >= 1 stay in key order (non-overlapping)
+            bisect.insort(lst, f, key=lambda x: x.smallest)
+
+    def version_files(self):
+        files = []
+        for lv, lst in enumerate(self.levels):
+            for f in lst:
+                files.append(dlsm_amd.VersionFile(lv, f.number, W.dbbench_keys_np(f.values[:1]).tobytes(),
+                                                  W.dbbench_keys_np(f.values[-1:]).tobytes(),
+                                                  (1 << 8) | 1, f.filter))
+        return files
+
+
+def run(num: int, threads: int, bpk: int, device: int = 0, reps: int = 1, read_batch: int = 25_000_000,
+        on_build=None, on_read=None):
     import torch
 
     ctx = dlsm_amd.Context(device)
     t0 = time.time()
     fill = fill_stream(num, threads)
     mem = flushes(fill)
-    tables = [dlsm_amd.Keys(W.dbbench_keys_np(v), v.size, 20) for v in mem]
     gen_s = time.time() - t0
-    n_fill_keys = int(sum(v.size for v in mem))
 
-    # ---- fillrandom: every flush's filter, host keys -> host slots -------
-    filters = ctx.full_build(tables, bpk)  # warm (allocations)
+    # ---- fillrandom: flushes + leveled compactions, every filter on the GPU --
+    lsm = LSM(ctx, bpk, on_build)
+    ctx.full_build([dlsm_amd.Keys(W.dbbench_keys_np(mem[0]), mem[0].size, 20)], bpk)  # warm-up (allocations)
     t1 = time.perf_counter()
-    for _ in range(reps):
-        filters = ctx.full_build(tables, bpk)
-    build_s = (time.perf_counter() - t1) / reps
+    for v in mem:
+        lsm.flush(v)
+    fill_wall_s = time.perf_counter() - t1
+    st = lsm.stats
 
-    # ---- readrandom: Gets over the level-0 flush files ---------------------
-    files = [dlsm_amd.VersionFile(0, j + 1, bytes(t.data[:20]), bytes(t.data[-20:]), (1 << 8) | 1, f)
-             for j, (t, f) in enumerate(zip(tables, filters))]
+    # ---- readrandom: Gets over the final version -------------------------
+    files = lsm.version_files()
     ver = ctx.version(files)
     reads = read_stream(num, threads)
-    q = W.dbbench_keys_np(reads)
     nq = reads.size
     dev = torch.device(f"cuda:{device}")
-    qh = torch.from_numpy(q).pin_memory()
-    mh = torch.empty(nq, dtype=torch.int64).pin_memory()
-    qd = torch.empty(q.size, dtype=torch.uint8, device=dev)
-    md = torch.empty(nq, dtype=torch.int64, device=dev)
+    B = min(read_batch, nq)
+    qh = torch.empty(B * 20, dtype=torch.uint8).pin_memory()
+    mh = torch.empty(B, dtype=torch.int64).pin_memory()
+    qd = torch.empty(B * 20, dtype=torch.uint8, device=dev)
+    md = torch.empty(B, dtype=torch.int64, device=dev)
     stream = torch.cuda.Stream(device=dev)
     ctx.set_stream(stream)
-
-    def get_batch():
+    read_s, probe_ms, hits = 0.0, 0.0, 0
+    for b0 in range(0, nq, B):
+        nb = min(B, nq - b0)
+        qh[: nb * 20].numpy()[:] = W.dbbench_keys_np(reads[b0:b0 + nb])
+        t2 = time.perf_counter()
         with torch.cuda.stream(stream):
-            qd.copy_(qh, non_blocking=True)
-            ctx.version_probe_dev(ver, dlsm_amd.Keys(qd, nq, 20), (1 << 56) - 1, md)
-            mh.copy_(md, non_blocking=True)
+            qd[: nb * 20].copy_(qh[: nb * 20], non_blocking=True)
+            ctx.version_probe_dev(ver, dlsm_amd.Keys(qd, nb, 20), (1 << 56) - 1, md)
+            mh[:nb].copy_(md[:nb], non_blocking=True)
         stream.synchronize()
-
-    get_batch()
-    t2 = time.perf_counter()
-    for _ in range(reps):
-        get_batch()
-    read_s = (time.perf_counter() - t2) / reps
-    # device-resident probe alone
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(reps):
-        ctx.version_probe_dev(ver, dlsm_amd.Keys(qd, nq, 20), (1 << 56) - 1, md)
-    ev1.record(stream)
-    stream.synchronize()
-    probe_dev_ms = ev0.elapsed_time(ev1) / reps
-    masks = mh.numpy().view(np.uint64)
-    hits = int(np.count_nonzero(masks))
-    filter_checks = len(mem) * nq  # what per-key Gets would do: every L0 file whose range holds the key
+        read_s += time.perf_counter() - t2
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        ctx.version_probe_dev(ver, dlsm_amd.Keys(qd, nb, 20), (1 << 56) - 1, md)  # device-resident alone
+        ev1.record(stream)
+        stream.synchronize()
+        probe_ms += ev0.elapsed_time(ev1)
+        m = mh[:nb].numpy().view(np.uint64)
+        hits += int(np.count_nonzero(m))
+        if on_read:
+            on_read(b0, reads[b0:b0 + nb], m.copy(), files)
     ctx.set_stream(None)
     ver.close()
+    built_keys = st["flush_keys"] + st["compaction_keys"]
+    build_s = st["flush_s"] + st["compaction_s"]
     return {
-        "workload": "db_bench fillrandom,readrandom replay (filter path), host buffers",
+        "workload": "db_bench fillrandom,readrandom replay (filter path, leveled compaction model), host buffers",
         "num": num, "threads": threads, "bloom_bits": bpk, "value_size": 400,
         "memtable_entries": MEMTABLE_ENTRIES, "flushes": len(mem),
-        "fill": {"writes": int(fill.size), "distinct_keys_flushed": n_fill_keys,
-                 "build_ms": round(build_s * 1e3, 3),
-                 "mkeys_s_incl_h2d_d2h": round(n_fill_keys / build_s / 1e6, 1),
-                 "filter_bytes": int(sum(len(f) for f in filters))},
-        "read": {"gets": int(nq), "ms": round(read_s * 1e3, 3),
+        "fill": {"writes": int(fill.size), "wall_s": round(fill_wall_s, 2),
+                 "flush_builds": st["flush_builds"], "flush_keys": st["flush_keys"],
+                 "compactions": st["compactions"], "trivial_moves": st["trivial_moves"],
+                 "compaction_builds": st["compaction_builds"], "compaction_keys": st["compaction_keys"],
+                 "filter_build_s_incl_h2d_d2h": round(build_s, 3),
+                 "filter_mkeys_s_incl_h2d_d2h": round(built_keys / build_s / 1e6, 1),
+                 "flush_filter_mkeys_s": round(st["flush_keys"] / max(st["flush_s"], 1e-9) / 1e6, 1),
+                 "compaction_filter_mkeys_s": round(st["compaction_keys"] / max(st["compaction_s"], 1e-9) / 1e6, 1),
+                 "host_merge_s": round(st["merge_s"], 2)},
+        "version": {"files_per_level": [len(l) for l in lsm.levels],
+                    "keys_per_level": [int(sum(f.values.size for f in l)) for l in lsm.levels]},
+        "read": {"gets": int(nq), "s_incl_h2d_d2h": round(read_s, 3),
                  "mgets_s_incl_h2d_d2h": round(nq / read_s / 1e6, 1),
-                 "probe_dev_ms": round(probe_dev_ms, 3),
-                 "mgets_s_device": round(nq / probe_dev_ms / 1e3, 1),
-                 "keys_with_a_candidate": hits, "l0_files_per_get": len(mem)},
+                 "probe_dev_ms": round(probe_ms, 3),
+                 "mgets_s_device": round(nq / probe_ms / 1e3, 1),
+                 "gets_with_a_candidate": hits},
         "host_keygen_s": round(gen_s, 1),
-    }, (mem, filters, reads, masks)
+    }, lsm
 
 
 def main():
@@ -144,11 +289,10 @@ def main():
     ap.add_argument("--num", type=int, default=500_000, help="db_bench --num (per thread)")
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--bloom-bits", type=int, default=10)
-    ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     if not dlsm_amd.device_available():
         raise SystemExit("dbbench_replay: no HIP device")
-    res, _ = run(args.num, args.threads, args.bloom_bits, reps=args.reps)
+    res, _ = run(args.num, args.threads, args.bloom_bits)
     print(json.dumps(res), flush=True)
 
 

@@ -34,7 +34,7 @@ PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
 INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbformat.h:374-377)
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
-OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG = 3, 4
+OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT = 3, 4, 5
 
 
 def lib():
@@ -253,6 +253,10 @@ class Context:
         """Job groups of a pipelined build (0 = auto, 1..4)."""
         self.set_option(OPT_BUILD_GROUPS, groups)
 
+    def set_build_exact(self, mode: int):
+        """0 auto, 1 count distinct hashes before bucketing, 2 never (DLSM_OPT_BUILD_EXACT)."""
+        self.set_option(OPT_BUILD_EXACT, mode)
+
     def set_probe_shape(self, chunk_lg: int, slice_lg: int):
         """Sliced probe shape: 2^chunk_lg keys per partition chunk (12..14),
         2^slice_lg stacked lines per LDS slice (7 = 64 KiB, 8 = 128 KiB)."""
@@ -270,6 +274,12 @@ class Context:
 
     def reserve(self, max_keys: int, max_jobs: int):
         check(lib().dlsm_ctx_reserve(self.h, max_keys, max_jobs), "reserve")
+
+    def stats(self):
+        """(device allocations made so far, workspace bytes held)."""
+        n, b = C.c_uint64(), C.c_uint64()
+        check(lib().dlsm_ctx_stats(self.h, C.byref(n), C.byref(b)), "stats")
+        return int(n.value), int(b.value)
 
     # -- full filter build --------------------------------------------------
     @staticmethod

@@ -68,10 +68,14 @@ SIGNATURES = [
     ("dlsm_ctx_stream", _VP, [_VP]),
     ("dlsm_ctx_sync", C.c_int, [_VP]),
     ("dlsm_ctx_reserve", C.c_int, [_VP, C.c_uint64, C.c_uint32]),
+    ("dlsm_ctx_stats", C.c_int, [_VP, _U64P, _U64P]),
     ("dlsm_ctx_set_path", C.c_int, [_VP, C.c_int]),
     ("dlsm_ctx_set_option", C.c_int, [_VP, C.c_int, C.c_uint64]),
     ("dlsm_host_register", C.c_int, [_VP, C.c_size_t]),
     ("dlsm_host_unregister", C.c_int, [_VP]),
+    ("dlsm_host_alloc", C.c_int, [C.c_size_t, C.POINTER(_VP)]),
+    ("dlsm_host_free", C.c_int, [_VP]),
+    ("dlsm_ctx_host_buffer", C.c_int, [_VP, C.c_uint64, C.c_uint64, C.POINTER(_VP), _U64P]),
     ("dlsm_bloom_full_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_bloom_full_build_block_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),

@@ -39,9 +39,11 @@ int from_hip(hipError_t e) {
 template <typename T>
 struct DevBuf {
   T* p = nullptr;
-  size_t cap = 0;  // elements
+  size_t cap = 0;     // elements
+  uint64_t gen = 0;   // bumped by every (re)allocation: contents are gone
   int ensure(size_t n) {
     if (n <= cap && p) return DLSM_OK;
+    gen++;
     if (p) {
       (void)hipFree(p);
       p = nullptr;
@@ -93,6 +95,7 @@ struct dlsm_ctx {
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14; 13 = two 4,096-key units, 512 threads)
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
+  int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -100,9 +103,13 @@ struct dlsm_ctx {
   DevBuf<uint32_t> starts;  // chunk0s | slice0s
   DevBuf<uint32_t> dchunk;  // per-chunk consecutive-distinct counts
   DevBuf<uint32_t> jobL;    // per-job line count (direct path)
-  // last uploaded job table (skip the H2D when a caller repeats a batch)
+  // last uploaded job table (skip the H2D when a caller repeats a batch); the
+  // device buffers' allocation generations are part of the key, so a buffer
+  // that ensure() reallocated (reserve, a bigger batch) -- even at the same
+  // address -- is never taken as filled
   std::vector<FullJobDev> last_jobs;
   std::vector<uint32_t> last_starts;
+  uint64_t last_jobs_gen = 0, last_starts_gen = 0;
   DevBuf<LegacyJobDev> ljobs;
   DevBuf<uint64_t> lstarts;
   // probe workspace
@@ -122,6 +129,9 @@ struct dlsm_ctx {
   DevBuf<uint32_t> crc_val;
   // internal-key selection / gather: [blk_cnt | blk_bytes | tot(2) | first_bad]
   DevBuf<uint64_t> sel;
+  // page-locked host staging lent to the context's (single) builder
+  void* host_buf = nullptr;
+  uint64_t host_cap = 0;
 };
 
 struct dlsm_filterset {
@@ -370,6 +380,7 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   }
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
   delete ctx;
   return DLSM_OK;
 }
@@ -415,6 +426,10 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value < 7 || value > 8) return DLSM_E_ARG;
       ctx->probe_lgr = static_cast<int>(value);
       return DLSM_OK;
+    case DLSM_OPT_BUILD_EXACT:
+      if (value > 2) return DLSM_E_ARG;
+      ctx->build_exact = static_cast<int>(value);
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -441,6 +456,23 @@ int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   return DLSM_OK;
 }
 
+int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_bytes) {
+  if (!ctx) return DLSM_E_ARG;
+  uint64_t n = 0, b = 0;
+  auto add = [&](const auto& buf) {
+    n += buf.gen;
+    b += buf.cap * sizeof(*buf.p);
+  };
+  add(ctx->entries); add(ctx->tab); add(ctx->jobs); add(ctx->starts); add(ctx->dchunk);
+  add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->pos); add(ctx->smask);
+  add(ctx->st_keys); add(ctx->st_offs); add(ctx->st_out); add(ctx->st_len); add(ctx->st_filter);
+  add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_outp); add(ctx->crc_cap);
+  add(ctx->crc_val); add(ctx->sel);
+  if (device_allocs) *device_allocs = n;
+  if (device_bytes) *device_bytes = b;
+  return DLSM_OK;
+}
+
 int dlsm_host_register(void* p, size_t len) {
   if (!p || !len) return DLSM_E_ARG;
   DLSM_TRY(hipHostRegister(p, len, hipHostRegisterDefault));
@@ -450,6 +482,40 @@ int dlsm_host_register(void* p, size_t len) {
 int dlsm_host_unregister(void* p) {
   if (!p) return DLSM_E_ARG;
   DLSM_TRY(hipHostUnregister(p));
+  return DLSM_OK;
+}
+
+int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes, void** out,
+                         uint64_t* cap) {
+  if (!ctx || !out || keep_bytes > ctx->host_cap) return DLSM_E_ARG;
+  if (min_bytes > ctx->host_cap || !ctx->host_buf) {
+    uint64_t c = std::max<uint64_t>(ctx->host_cap ? 2 * ctx->host_cap : (uint64_t(1) << 20), min_bytes);
+    void* p = nullptr;
+    DLSM_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
+    if (keep_bytes) memcpy(p, ctx->host_buf, keep_bytes);
+    if (ctx->host_buf) {
+      // the previous buffer may still be the source of a queued copy
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipHostFree(ctx->host_buf);
+    }
+    ctx->host_buf = p;
+    ctx->host_cap = c;
+  }
+  *out = ctx->host_buf;
+  if (cap) *cap = ctx->host_cap;
+  return DLSM_OK;
+}
+
+int dlsm_host_alloc(size_t len, void** out) {
+  if (!out || !len) return DLSM_E_ARG;
+  *out = nullptr;
+  DLSM_TRY(hipHostMalloc(out, len, hipHostMallocDefault));
+  return DLSM_OK;
+}
+
+int dlsm_host_free(void* p) {
+  if (!p) return DLSM_OK;
+  DLSM_TRY(hipHostFree(p));
   return DLSM_OK;
 }
 
@@ -477,6 +543,17 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   if (lgR < 0) sliced_ok = false;
   if (ctx->path == 2 && !sliced_ok) return DLSM_E_ARG;
   const int mode = all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC);
+  // Exact line counts (a count pass before the partition) where duplicate
+  // user keys are expected to lower L below the speculative n-key count:
+  // internal keys (several versions of a user key, suffix_len 8) and the
+  // per-key-length batches a TableBuilder adapter hands over.  The
+  // device-resident fixed-length user-key batches (one entry per user key)
+  // stay speculative: one pass over the keys, with a per-slice re-hash
+  // fallback for the rare batch whose duplicates do change L.
+  bool any_suffix = false;
+  for (int j = 0; j < n_jobs; j++) any_suffix = any_suffix || jobs[j].keys.suffix_len > 0;
+  const bool exact = sliced_ok && (ctx->build_exact == 1 ||
+                                   (ctx->build_exact == 0 && (any_suffix || mode == KM_GENERIC)));
 
   std::vector<FullJobDev> hj(n_jobs);
   std::vector<uint32_t> starts(2 * n_jobs);
@@ -499,6 +576,8 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     d.tab0 = tabw;
     d.k = k;
     d.bpk = bits_per_key;
+    d.exact = exact ? 1 : 0;
+    d.reserved = 0;
     starts[j] = chunk;
     starts[n_jobs + j] = slice;
     entry += (b.keys.n + 15) & ~uint64_t(15);  // 16-element aligned: 16-byte stores
@@ -509,8 +588,10 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   hipStream_t s = ctx->stream;
   const bool same = ctx->last_jobs.size() == hj.size() && ctx->last_starts == starts &&
                     memcmp(ctx->last_jobs.data(), hj.data(), sizeof(FullJobDev) * n_jobs) == 0 &&
+                    ctx->jobs.gen == ctx->last_jobs_gen && ctx->starts.gen == ctx->last_starts_gen &&
                     ctx->jobs.cap >= static_cast<size_t>(n_jobs);
   if (!same) {
+    ctx->last_jobs.clear();  // until the upload below is queued
     DLSM_CHECK(ctx->jobs.ensure(n_jobs));
     DLSM_CHECK(ctx->starts.ensure(2 * n_jobs));
     DLSM_TRY(hipMemcpyAsync(ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs,
@@ -519,6 +600,8 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
                             hipMemcpyHostToDevice, s));
     ctx->last_jobs = hj;
     ctx->last_starts = starts;
+    ctx->last_jobs_gen = ctx->jobs.gen;
+    ctx->last_starts_gen = ctx->starts.gen;
   }
   DLSM_CHECK(ctx->dchunk.ensure(chunk));
   DLSM_CHECK(ctx->jobL.ensure(n_jobs));
@@ -538,11 +621,12 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     const int ng = static_cast<int>(cut.size()) - 1;
     auto chunk_at = [&](int j) { return j < n_jobs ? starts[j] : chunk; };
     auto slice_at = [&](int j) { return j < n_jobs ? starts[n_jobs + j] : slice; };
+    if (exact) DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, s));
     if (ng > 1) DLSM_CHECK(fork_aux(ctx));
     for (int g = 0; g < ng; g++) {
       const uint32_t c0 = chunk_at(cut[g]), s0 = slice_at(cut[g]);
       DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, c0, chunk_at(cut[g + 1]) - c0,
-                                     ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, mode,
+                                     ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, mode, exact,
                                      ng > 1 ? ctx->aux : s));
       if (ng > 1) DLSM_CHECK(hand_over(ctx->aux, s, ctx->ev_part[g % kStageEvents]));
       DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, s0, slice_at(cut[g + 1]) - s0,
@@ -645,20 +729,26 @@ int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
 // ---------------------------------------------------------------------------
 // Filter blocks (build + crc32c trailer) and crc32c of device buffers
 // ---------------------------------------------------------------------------
-uint32_t dlsm_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
-  static uint32_t table[256];
-  static bool init = false;
-  if (!init) {
+namespace {
+struct Crc32cTable {
+  uint32_t t[256];
+  Crc32cTable() {
     for (uint32_t i = 0; i < 256; i++) {
       uint32_t c = i;
       for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0x82f63b78u : (c >> 1);
-      table[i] = c;
+      t[i] = c;
     }
-    init = true;
   }
+};
+}  // namespace
+
+uint32_t dlsm_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  // function-local static: C++11 thread-safe initialisation (TableBuilders
+  // seal blocks from several threads)
+  static const Crc32cTable table;
   const uint8_t* p = static_cast<const uint8_t*>(data);
   uint32_t c = ~init_crc;
-  for (size_t i = 0; i < n; i++) c = table[(c ^ p[i]) & 0xffu] ^ (c >> 8);
+  for (size_t i = 0; i < n; i++) c = table.t[(c ^ p[i]) & 0xffu] ^ (c >> 8);
   return ~c;
 }
 

@@ -37,6 +37,11 @@ struct FullJobDev {
   uint32_t slice0, n_slices;
   uint32_t L_spec, magic_spec;  // speculative line count (no duplicates) + fastmod magic
   int32_t k, bpk;
+  // 1: a count pass ran first (dchunk holds every chunk's distinct count), so
+  // the partition buckets by the true line count, not L_spec -- batches whose
+  // duplicates lower L (internal keys with several versions per user key)
+  int32_t exact;
+  int32_t reserved;
 };
 
 // A parsed full filter resident on the device (FullFilterBlockReader state).
@@ -99,9 +104,11 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
                                uint32_t total_chunks, const uint32_t* jobL, int mode, hipStream_t s);
 // Partition chunks [chunk_first, +n_chunks) / slices [slice_first, +n_slices)
 // of the job table (a contiguous job group of a pipelined build).
+// exact: the count pass already filled dchunk; bucket by each job's true line count.
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                  uint32_t chunk_first, uint32_t n_chunks, uint32_t* dchunk,
-                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, hipStream_t s);
+                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, bool exact,
+                                 hipStream_t s);
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
                               const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "bloom_internal.h"
@@ -641,7 +642,15 @@ __device__ __forceinline__ uint32_t build_entry_off(uint32_t e) {
 #endif
 constexpr int kPartBlock = kBuildChunk / 8;  // 8 keys per thread (512 threads at 4,096-key chunks)
 
-template <int MODE, bool PART>
+// Job-wide distinct count (defined below; used by the exact partition).
+template <int NT>
+__device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint32_t* dchunk,
+                                                 uint32_t* wsum64);
+
+// EXACT (PART only): the count pass already wrote every chunk's distinct count
+// to dchunk, so each workgroup sums its job's counts and buckets by the true
+// line count instead of the speculative one.
+template <int MODE, bool PART, bool EXACT = false>
 __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
     uint32_t* __restrict__ dchunk, uint32_t* __restrict__ entries, uint16_t* __restrict__ tab,
@@ -670,12 +679,18 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   // the key before the chunk (AddKey's dedup neighbour), hashed before the
   // chunk's tile loads so its round trip overlaps them
   uint32_t prev_h = 0;
-  if (first > 0 && tid == 0) prev_h = key_hash<MODE>(J.keys, first - 1);  // only wave 0 lane 0 reads it
+  if (!EXACT && first > 0 && tid == 0) prev_h = key_hash<MODE>(J.keys, first - 1);  // only wave 0 lane 0 reads it
   uint32_t h[PER];
   hash_chunk<MODE, kPartBlock, PER>(J.keys, first, nk, tile, h);
-  const uint32_t prev0 = first > 0 ? __shfl(prev_h, 0, 64) : ~__shfl(h[0], 0, 64);
-  const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, prev0, lastw, wsum);
-  if (tid == 0) dchunk[bid] = cnt;
+  uint32_t L = J.L_spec, magic = J.magic_spec;
+  if constexpr (EXACT) {
+    L = full_num_lines(job_distinct<kPartBlock>(J, dchunk, wsum), J.bpk, nullptr);
+    magic = fastmod_magic(L);
+  } else {
+    const uint32_t prev0 = first > 0 ? __shfl(prev_h, 0, 64) : ~__shfl(h[0], 0, 64);
+    const uint32_t cnt = chunk_distinct<kPartBlock, PER>(h, nk, prev0, lastw, wsum);
+    if (tid == 0) dchunk[bid] = cnt;
+  }
   if constexpr (!PART) return;
 
   const uint32_t S = J.n_slices;
@@ -686,7 +701,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) {
-      const uint32_t line = fastmod(h[r], J.L_spec, J.magic_spec);
+      const uint32_t line = fastmod(h[r], L, magic);
       const uint32_t s = line >> lgR;
       code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
 #if DLSM_BUILD_LINE_IN_ENTRY
@@ -712,6 +727,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
 template <int NT>
 __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint32_t* dchunk,
                                                  uint32_t* wsum64) {
+  __syncthreads();  // wsum64 may still be read from a previous use
   uint32_t lo = 0;
   for (uint32_t c = threadIdx.x; c < J.n_chunks; c += NT) lo += dchunk[J.chunk0 + c];
   // chunk counts are <= 4096, so a 32-bit partial per thread cannot overflow
@@ -785,7 +801,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
   const uint32_t lo_line = s << LGR;
   if (L != 0 && lo_line < L) {
     const uint32_t magic = fastmod_magic(L);
-    if (L == J.L_spec) {
+    if (L == J.L_spec || J.exact) {  // the partition bucketed by this L
       const uint32_t nC = J.n_chunks;
       const uint16_t* tb = tab + J.tab0 + s;  // chunk-major rows of n_slices+1 u16
       const uint32_t* ent = entries + J.entry0;
@@ -1211,7 +1227,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
 // (16-byte loads), gather them back to key order through pos (16-byte loads
 // of 8 positions), store 8 answers per lane.
-template <int C>
+// VEC: 8-byte answer stores (mask 8-byte aligned); otherwise byte stores, for
+// a caller's mask that starts anywhere (a sub-slice of a byte tensor).
+template <int C, bool VEC>
 __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
                                                                  const uint16_t* __restrict__ pos,
                                                                  const uint8_t* __restrict__ smask,
@@ -1239,7 +1257,15 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
         hi |= uint32_t(sm[pw[q + 2] & 0xffffu]) << (16 * q);
         hi |= uint32_t(sm[pw[q + 2] >> 16]) << (16 * q + 8);
       }
-      *reinterpret_cast<uint2*>(mask + first + i0) = make_uint2(lo, hi);
+      if constexpr (VEC) {
+        *reinterpret_cast<uint2*>(mask + first + i0) = make_uint2(lo, hi);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          mask[first + i0 + b] = static_cast<uint8_t>(lo >> (8 * b));
+          mask[first + i0 + 4 + b] = static_cast<uint8_t>(hi >> (8 * b));
+        }
+      }
     } else {
       for (uint32_t i = i0; i < nk; i++) mask[first + i] = sm[pos[first + i]];
     }
@@ -1423,17 +1449,20 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
 
 hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                  uint32_t chunk_first, uint32_t n_chunks, uint32_t* dchunk,
-                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, hipStream_t s) {
+                                 uint32_t* entries, uint16_t* tab, int lgR, int mode, bool exact,
+                                 hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
-  if (mode == KM_K20)
-    full_partition_kernel<KM_K20, true><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
-                                                                     entries, tab, lgR, chunk_first);
-  else if (mode == KM_K28)
-    full_partition_kernel<KM_K28, true><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
-                                                                     entries, tab, lgR, chunk_first);
-  else
-    full_partition_kernel<KM_GENERIC, true><<<n_chunks, kPartBlock, 0, s>>>(
-        jobs, chunk0s, n_jobs, dchunk, entries, tab, lgR, chunk_first);
+#define DLSM_PART(MM, EX)                                                                   \
+  full_partition_kernel<MM, true, EX><<<n_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, \
+                                                                      dchunk, entries, tab, lgR, chunk_first)
+  if (mode == KM_K20) {
+    if (exact) DLSM_PART(KM_K20, true); else DLSM_PART(KM_K20, false);
+  } else if (mode == KM_K28) {
+    if (exact) DLSM_PART(KM_K28, true); else DLSM_PART(KM_K28, false);
+  } else {
+    if (exact) DLSM_PART(KM_GENERIC, true); else DLSM_PART(KM_GENERIC, false);
+  }
+#undef DLSM_PART
   return hipGetLastError();
 }
 
@@ -1486,17 +1515,20 @@ hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, 
   return hipGetLastError();
 }
 
-// Compute units of the current device (cached per device id).
+// Compute units of the current device (cached per device id; builder threads
+// call this concurrently, so the cache is atomic).
 static uint32_t device_cus() {
-  static uint32_t cus[64] = {};
+  static std::atomic<uint32_t> cus[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256u;
-  if (!cus[dev]) {
+  uint32_t c = cus[dev].load(std::memory_order_relaxed);
+  if (!c) {
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cus[dev] = static_cast<uint32_t>(n);
+    c = static_cast<uint32_t>(n);
+    cus[dev].store(c, std::memory_order_relaxed);
   }
-  return cus[dev];
+  return c;
 }
 
 #ifndef DLSM_PROBE_P13_HALF
@@ -1588,12 +1620,17 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
                                   uint8_t* mask, int lgC, hipStream_t s) {
   if (n_keys == 0) return hipSuccess;
   const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
+  const bool vec = (reinterpret_cast<uintptr_t>(mask) & 7u) == 0;
+#define DLSM_UNPERMUTE(CC)                                                         \
+  if (vec) probe_unpermute_kernel<CC, true><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); \
+  else probe_unpermute_kernel<CC, false><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask)
   switch (lgC) {
-    case 12: probe_unpermute_kernel<4096><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
-    case 13: probe_unpermute_kernel<8192><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
-    case 14: probe_unpermute_kernel<16384><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask); break;
+    case 12: DLSM_UNPERMUTE(4096); break;
+    case 13: DLSM_UNPERMUTE(8192); break;
+    case 14: DLSM_UNPERMUTE(16384); break;
     default: return hipErrorInvalidValue;
   }
+#undef DLSM_UNPERMUTE
   return hipGetLastError();
 }
 

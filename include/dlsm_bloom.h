@@ -119,6 +119,11 @@ void* dlsm_ctx_stream(dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
 /* Pre-size the device workspace so later calls never allocate (graph capture). */
 int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs);
+/* Workspace statistics: device allocations the context has made so far
+ * (every growth of a workspace buffer counts one) and the bytes it holds.
+ * After dlsm_ctx_reserve (or one warm-up call of each shape) the count stays
+ * put: the hot path does not allocate. */
+int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_bytes);
 /* Select kernels: 0 = auto, 1 = direct (global atomics / global probes),
  * 2 = sliced (LDS-tiled).  For A/B measurement; results are identical. */
 int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
@@ -131,18 +136,37 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *   DLSM_OPT_PROBE_CHUNK_LG   log2 keys per probe partition chunk, 12..14 (default 13,
  *                             or $DLSM_PROBE_CHUNK_LG)
  *   DLSM_OPT_PROBE_SLICE_LG   log2 stacked filter lines per probe LDS slice, 7 (64 KiB)
- *                             or 8 (128 KiB) (default 8, or $DLSM_PROBE_SLICE_LG) */
+ *                             or 8 (128 KiB) (default 8, or $DLSM_PROBE_SLICE_LG)
+ *   DLSM_OPT_BUILD_EXACT      0 auto (default): count consecutive-distinct hashes in a
+ *                             pass of their own before bucketing when the batch has
+ *                             internal keys (suffix_len > 0) or per-key lengths (offsets),
+ *                             whose duplicate user keys lower the line count; 1 always;
+ *                             2 never (one pass; a batch whose duplicates change the line
+ *                             count then takes a slower per-slice re-hash fallback) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
 #define DLSM_OPT_PROBE_CHUNK_LG 3
 #define DLSM_OPT_PROBE_SLICE_LG 4
+#define DLSM_OPT_BUILD_EXACT 5
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 
 /* Page-lock a host range (e.g. an RDMA-registered FilterChunk slot) so D2H
  * copies land in it directly. */
 int dlsm_host_register(void* p, size_t len);
 int dlsm_host_unregister(void* p);
+/* Page-locked host allocation (the H2D / D2H of the host-memory calls then
+ * run as DMA at the link rate). */
+int dlsm_host_alloc(size_t len, void** out);
+int dlsm_host_free(void* p);
+/* The context's own page-locked host staging buffer, lent to the builder that
+ * uses the context (one at a time: the reference runs one TableBuilder per
+ * thread, one context per thread): at least min_bytes; when it has to grow,
+ * its first keep_bytes bytes move to the new buffer.  Valid until the next
+ * call that grows it or dlsm_ctx_destroy.  Builders created per SSTable reuse
+ * it, so key staging allocates nothing after the first table. */
+int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes, void** out,
+                         uint64_t* cap);
 
 /* ---- full filter (SSTable format), build -------------------------------- */
 

@@ -1,21 +1,33 @@
 // dlsm_bloom_adapter.hpp -- header-only C++ mirror of dLSM's filter classes
 // over the C ABI (dlsm_bloom.h).  Same class and method names, argument
-// meaning and call order as the reference, so a TableBuilder / Table can swap
-// them in (INTEGRATION.md shows the reference-side edit):
+// meaning and call order as the reference, so a TableBuilder / Table / DB
+// can swap them in (INTEGRATION.md shows the reference-side edit):
 //
+//   FilterPolicy            include/TimberSaw/filter_policy.h:31-55
+//       the abstract interface (virtual Name / CreateFilter / KeyMayMatch)
+//   BloomFilterPolicy       util/bloom.cc:14-91 (: FilterPolicy),
+//       NewBloomFilterPolicy util/bloom.cc:89-91
+//   InternalFilterPolicy    db/dbformat.h:399-408, db/dbformat.cc:93-109
+//       (: FilterPolicy) -- internal keys, hashed as ExtractUserKey(key)
 //   FullFilterBlockBuilder  table/full_filter_block.h:33-70
 //       (RestartBlock AddKey*)* Finish; Reset; Move_buffer; public `result`
 //   FullFilterBlockReader   table/full_filter_block.h:71-94
 //       ctor parses metadata; KeyMayMatch; + KeysMayMatch (batch)
-//   BloomFilterPolicy       include/TimberSaw/filter_policy.h:31-55, util/bloom.cc
-//       Name / CreateFilter / KeyMayMatch
 //   FilterBlockBuilder      table/filter_block.h:34-68 (legacy 2 KiB framing)
 //       StartBlock AddKey* ... Finish; public `result`
 //   FilterBlockReader       table/filter_block.h:70-85
 //       KeyMayMatch(block_offset, key) + KeysMayMatch (batch)
 //
-// No exceptions (the reference builds with -fno-exceptions): failures are
-// reported through status().  All compute runs on the GPU behind the ABI.
+// Host types.  By default the header declares its own Slice and FilterPolicy
+// with the reference's surface.  Inside the reference tree, define
+// DLSM_ADAPTER_HOST_NAMESPACE to the host's namespace (TimberSaw) before
+// including it: the adapter then uses TimberSaw::Slice and derives from
+// TimberSaw::FilterPolicy, so a BloomFilterPolicy / InternalFilterPolicy from
+// here can be stored in Options::filter_policy (options.h:185-187).
+//
+// No exceptions and no RTTI (the reference builds with -fno-exceptions
+// -fno-rtti): failures are reported through status().  All compute runs on
+// the GPU behind the ABI.
 #pragma once
 
 #include <cstddef>
@@ -28,6 +40,10 @@
 
 namespace dlsm_adapter {
 
+#ifdef DLSM_ADAPTER_HOST_NAMESPACE
+using Slice = ::DLSM_ADAPTER_HOST_NAMESPACE::Slice;
+using FilterPolicy = ::DLSM_ADAPTER_HOST_NAMESPACE::FilterPolicy;
+#else
 // Byte view with the reference Slice's surface used on this path
 // (include/TimberSaw/slice.h:27-103): data/size/Reset/append.
 class Slice {
@@ -54,51 +70,124 @@ class Slice {
   size_t size_;
 };
 
+// include/TimberSaw/filter_policy.h:31-55
+class FilterPolicy {
+ public:
+  virtual ~FilterPolicy() {}
+  virtual const char* Name() const = 0;
+  // Append a filter summarising keys[0, n) to *dst (initial contents kept).
+  virtual void CreateFilter(const Slice* keys, int n, Slice* dst) const = 0;
+  virtual bool KeyMayMatch(const Slice& key, const Slice& filter) const = 0;
+};
+#endif
+
+// db/dbformat.h:374-377 (asserts internal_key.size() >= 8).
+inline Slice ExtractUserKey(const Slice& internal_key) {
+  return Slice(internal_key.data(), internal_key.size() >= DLSM_INTERNAL_KEY_TRAILER
+                                        ? internal_key.size() - DLSM_INTERNAL_KEY_TRAILER
+                                        : 0);
+}
+
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
 struct FilterSlot {
   void* addr;
   size_t length;
 };
 
+// Key staging in the context's page-locked host buffer
+// (dlsm_ctx_host_buffer): AddKey writes the keys where Finish's H2D DMA reads
+// them, and builders created per SSTable reuse the context's buffer.
+class PinnedBytes {
+ public:
+  explicit PinnedBytes(dlsm_ctx* ctx) : ctx_(ctx) {}
+  PinnedBytes(const PinnedBytes&) = delete;
+  PinnedBytes& operator=(const PinnedBytes&) = delete;
+  bool append(const char* d, size_t n) {
+    if (size_ + n > cap_) {
+      void* q = nullptr;
+      uint64_t c = 0;
+      if (dlsm_ctx_host_buffer(ctx_, size_ + n, size_, &q, &c) != DLSM_OK) return false;
+      p_ = static_cast<uint8_t*>(q);
+      cap_ = c;
+    }
+    memcpy(p_ + size_, d, n);
+    size_ += n;
+    return true;
+  }
+  void clear() { size_ = 0; }
+  const uint8_t* data() const { return p_ ? p_ : reinterpret_cast<const uint8_t*>(""); }
+  size_t size() const { return size_; }
+
+ private:
+  dlsm_ctx* ctx_;
+  uint8_t* p_ = nullptr;
+  size_t size_ = 0, cap_ = 0;
+};
+
 class FullFilterBlockBuilder {
  public:
   FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx)
       : local_mr_(mr), bits_per_key_(bits_per_key),
-        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx),
-        result(static_cast<char*>(mr->addr), 0) {
-    offsets_.push_back(0);
-  }
+        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx), keys_(ctx),
+        result(static_cast<char*>(mr->addr), 0) {}
   FullFilterBlockBuilder(const FullFilterBlockBuilder&) = delete;
   FullFilterBlockBuilder& operator=(const FullFilterBlockBuilder&) = delete;
 
   // full_filter_block.cc:30-33 -- drops the pending keys.
-  void RestartBlock(uint64_t /*block_offset*/) {
-    keys_.clear();
-    offsets_.assign(1, 0);
-  }
+  void RestartBlock(uint64_t /*block_offset*/) { clear_keys(); }
   // full_filter_block.cc:39-49 -- the GPU applies the consecutive-hash dedup.
+  // The builder only records the keys (pinned staging) and whether they all
+  // have one length (then Finish hands them over as a fixed-stride set: the
+  // LDS-tiled key loaders) and whether a key repeats its predecessor (then
+  // the line count is counted exactly before bucketing: DLSM_OPT_BUILD_EXACT).
   void AddKey(const Slice& key) {
-    keys_.append(key.data(), key.size());
-    offsets_.push_back(keys_.size());
+    const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
+    if (n_ == 0) {
+      key_len_ = key.size();
+    } else {
+      if (key.size() == last_len_ && memcmp(keys_.data() + prev0, key.data(), last_len_) == 0) dups_++;
+      if (uniform_ && key.size() != key_len_) {  // first key of another length: offsets from now on
+        uniform_ = false;
+        offsets_.resize(n_ + 1);
+        for (uint64_t i = 0; i <= n_; i++) offsets_[i] = i * key_len_;
+      }
+    }
+    if (!keys_.append(key.data(), key.size())) status_ = DLSM_E_NOMEM;
+    if (!uniform_) offsets_.push_back(keys_.size());
+    last_len_ = key.size();
+    n_++;
   }
   // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
   // buffer (the slot, or the buffer given to Move_buffer).
   void Finish() {
+    if (status_ != DLSM_OK) {
+      result.Reset(result.data(), 0);
+      clear_keys();
+      return;
+    }
     dlsm_build_job job;
-    job.keys.bytes = reinterpret_cast<const uint8_t*>(keys_.data());
-    job.keys.offsets = offsets_.data();
-    job.keys.key_len = 0;
+    job.keys.bytes = keys_.data();
+    job.keys.n = n_;
     job.keys.suffix_len = 0;
-    job.keys.n = offsets_.size() - 1;
+    if (uniform_) {
+      job.keys.offsets = nullptr;
+      job.keys.key_len = static_cast<uint32_t>(key_len_);
+    } else {
+      job.keys.offsets = offsets_.data();
+      job.keys.key_len = 0;
+    }
     job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
     job.out_cap = local_mr_->length - static_cast<size_t>(result.data() - static_cast<char*>(local_mr_->addr));
     if (result.data() < static_cast<char*>(local_mr_->addr) ||
         result.data() >= static_cast<char*>(local_mr_->addr) + local_mr_->length)
       job.out_cap = moved_cap_;
     uint64_t len = 0;
+    // repeated keys lower the line count: have the library count it exactly
+    // first (this builder's context belongs to its thread)
+    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 1);
     status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
-    keys_.clear();
-    offsets_.assign(1, 0);
+    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 0);
+    clear_keys();
     result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
   void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
@@ -112,12 +201,22 @@ class FullFilterBlockBuilder {
   int status() const { return status_; }
 
  private:
+  void clear_keys() {
+    keys_.clear();
+    offsets_.clear();
+    uniform_ = true;
+    key_len_ = last_len_ = 0;
+    n_ = dups_ = 0;
+  }
   FilterSlot* local_mr_;
   int bits_per_key_;
   int num_probes_;
   dlsm_ctx* ctx_;
-  std::string keys_;
-  std::vector<uint64_t> offsets_;
+  PinnedBytes keys_;               // the keys, back to back
+  std::vector<uint64_t> offsets_;  // key boundaries, only once lengths differ
+  bool uniform_ = true;
+  size_t key_len_ = 0, last_len_ = 0;
+  uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = SIZE_MAX;
   int status_ = DLSM_OK;
 
@@ -174,15 +273,18 @@ class FullFilterBlockReader {
   int status_ = DLSM_OK;
 };
 
-// The legacy-format policy (util/bloom.cc).  Name() keeps the reference's
-// format identity string.
-class BloomFilterPolicy {
+// The legacy-format policy (util/bloom.cc:14-91) as a FilterPolicy.
+// Name() keeps the reference's format identity string.  suffix_len() = 8
+// makes it hash ExtractUserKey(key) of internal keys on the GPU (the form
+// InternalFilterPolicy wraps it in).
+class BloomFilterPolicy : public FilterPolicy {
  public:
-  BloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx) : bits_per_key_(bits_per_key), ctx_(ctx) {}
-  const char* Name() const { return "TimberSaw.BuiltinBloomFilter2"; }
+  BloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx, uint32_t suffix_len = 0)
+      : bits_per_key_(bits_per_key), ctx_(ctx), suffix_len_(suffix_len) {}
+  const char* Name() const override { return "TimberSaw.BuiltinBloomFilter2"; }
 
   // Append a filter summarising keys[0, n) to *dst (util/bloom.cc:25-55).
-  void CreateFilter(const Slice* keys, int n, Slice* dst) const {
+  void CreateFilter(const Slice* keys, int n, Slice* dst) const override {
     std::string bytes;
     std::vector<uint64_t> offs(1, 0);
     for (int i = 0; i < n; i++) {
@@ -192,7 +294,7 @@ class BloomFilterPolicy {
     uint64_t need = 0;
     dlsm_bloom_legacy_size(static_cast<uint64_t>(n < 0 ? 0 : n), bits_per_key_, &need);
     dlsm_build_job job;
-    job.keys = dlsm_keyset{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0,
+    job.keys = dlsm_keyset{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, suffix_len_,
                            static_cast<uint64_t>(n < 0 ? 0 : n)};
     job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(dst->data())) + dst->size();
     job.out_cap = need;
@@ -200,24 +302,67 @@ class BloomFilterPolicy {
     last_status_ = dlsm_bloom_legacy_build(ctx_, &job, 1, bits_per_key_, &len);
     if (last_status_ == DLSM_OK) dst->Reset(dst->data(), dst->size() + len);
   }
-  bool KeyMayMatch(const Slice& key, const Slice& filter) const {
-    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(key.data()), nullptr,
-                   static_cast<uint32_t>(key.size()), 0, 1};
+  bool KeyMayMatch(const Slice& key, const Slice& filter) const override {
+    static const uint8_t z = 0;
+    const uint64_t offs[2] = {0, key.size()};
+    dlsm_keyset ks{key.size() ? reinterpret_cast<const uint8_t*>(key.data()) : &z, offs, 0, suffix_len_, 1};
     uint8_t r = 0;
-    if (key.size() == 0) {
-      static const uint8_t z = 0;
-      ks.bytes = &z;
-    }
     last_status_ = dlsm_bloom_legacy_probe(ctx_, reinterpret_cast<const uint8_t*>(filter.data()),
                                            filter.size(), &ks, &r);
     return last_status_ == DLSM_OK && r != 0;
   }
+  int bits_per_key() const { return bits_per_key_; }
+  dlsm_ctx* ctx() const { return ctx_; }
+  uint32_t suffix_len() const { return suffix_len_; }
   int status() const { return last_status_; }
 
  private:
   int bits_per_key_;
   dlsm_ctx* ctx_;
+  uint32_t suffix_len_;
   mutable int last_status_ = DLSM_OK;
+};
+
+// util/bloom.cc:89-91; the caller deletes the result (after every DB using it
+// is closed), as with the reference.
+inline const FilterPolicy* NewBloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx) {
+  return new BloomFilterPolicy(bits_per_key, ctx);
+}
+
+// db/dbformat.h:399-408, db/dbformat.cc:93-109: converts internal keys to
+// user keys for the wrapped policy.
+//  * wrapping this header's BloomFilterPolicy: the internal keys go to the
+//    GPU as they are, with suffix_len = 8 -- the kernels hash
+//    ExtractUserKey(key), no host-side stripping pass;
+//  * wrapping any other FilterPolicy: keys[] is rewritten to the user keys
+//    and handed on, exactly as the reference does ("the code in table.cc
+//    does not mind us adjusting keys[]").
+// The reference rewrites keys[] in both cases; so does this class, so a
+// caller sees the same keys[] afterwards.
+class InternalFilterPolicy : public FilterPolicy {
+ public:
+  explicit InternalFilterPolicy(const FilterPolicy* p) : user_policy_(p) {}
+  explicit InternalFilterPolicy(const BloomFilterPolicy* p)
+      : user_policy_(p), gpu_(p->bits_per_key(), p->ctx(), DLSM_INTERNAL_KEY_TRAILER) {
+    gpu_ok_ = true;
+  }
+  const char* Name() const override { return user_policy_->Name(); }
+  void CreateFilter(const Slice* keys, int n, Slice* dst) const override {
+    if (gpu_ok_) gpu_.CreateFilter(keys, n, dst);
+    Slice* mkey = const_cast<Slice*>(keys);
+    for (int i = 0; i < n; i++) mkey[i] = ExtractUserKey(keys[i]);
+    if (!gpu_ok_) user_policy_->CreateFilter(keys, n, dst);
+  }
+  bool KeyMayMatch(const Slice& key, const Slice& f) const override {
+    if (gpu_ok_) return gpu_.KeyMayMatch(key, f);
+    return user_policy_->KeyMayMatch(ExtractUserKey(key), f);
+  }
+  int status() const { return gpu_ok_ ? gpu_.status() : DLSM_OK; }
+
+ private:
+  const FilterPolicy* const user_policy_;
+  BloomFilterPolicy gpu_{0, nullptr};
+  bool gpu_ok_ = false;
 };
 
 // table/filter_block.cc:14-113 with the legacy Bloom policy.  StartBlock /

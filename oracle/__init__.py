@@ -93,45 +93,72 @@ def lib():
     return _LIB
 
 
-def ref_timed_baseline(tables, n: int, filters: list, q: np.ndarray, nq: int, bpk: int,
-                       threads: int):
-    """Time the reference's own code (oracle/_ref/libref.so: util/bloom_impl.h
-    AddHash / HashMayMatch, util/hash.cc) on the host: one table per thread
-    for the build, lookups split over threads x every filter for the probe
-    (per-filter re-hash, as FullFilterBlockReader::KeyMayMatch does).  Returns
-    (build_s, probe_s, built filters, mask) or None without libref.so."""
+def timed_cpu_baseline(kind: str, tables, n: int, filters: list, q: np.ndarray, nq: int, bpk: int,
+                       threads: int, legacy_tables: int | None = None):
+    """Time the CPU path on the host: kind "reference" = the reference's own
+    code (oracle/_ref/libref.so: util/bloom_impl.h AddHash / HashMayMatch,
+    util/hash.cc, util/bloom.cc), kind "port" = this oracle's C restatement.
+    Cost structure of the reference: one SSTable per thread for the builds
+    (hash -> vector -> scatter, FullFilterBlockBuilder), the lookups split over
+    the threads with BloomHash recomputed per filter (FullFilterBlockReader::
+    KeyMayMatch), and util/bloom.cc CreateFilter (the legacy FilterPolicy
+    format) over the first `legacy_tables` tables.  Returns a dict of times
+    (s) and outputs, or None for "reference" without libref.so."""
     import time
     from concurrent.futures import ThreadPoolExecutor
 
-    R = ref_lib()
-    if R is None:
+    R = ref_lib() if kind == "reference" else None
+    if kind == "reference" and R is None:
         return None
+    L = lib()
     offs = np.arange(n + 1, dtype=np.uint64) * 20
     cap = full_filter_bytes(n, bpk)[0] + 64
+    lcap = int(L.orc_legacy_filter_bytes(n, bpk)) + 64
 
     def build_one(t):
         out = np.zeros(cap, dtype=np.uint8)
-        ln = R.ref_full_build(t.ctypes.data_as(C.c_char_p), _ptr(offs, u64p), n, bpk, out.ctypes.data, cap)
+        if R is not None:
+            ln = R.ref_full_build(t.ctypes.data_as(C.c_char_p), _ptr(offs, u64p), n, bpk, out.ctypes.data, cap)
+        else:
+            ln = L.orc_full_build(_ptr(t), None, 20, n, bpk, _ptr(out), cap)
+        return out[:ln].tobytes()
+
+    def legacy_one(t):
+        out = np.zeros(lcap, dtype=np.uint8)
+        if R is not None:
+            ln = R.ref_legacy_create(t.ctypes.data_as(C.c_char_p), _ptr(offs, u64p), n, bpk, out.ctypes.data)
+        else:
+            ln = L.orc_legacy_build(_ptr(t), None, 20, n, bpk, _ptr(out), lcap)
         return out[:ln].tobytes()
 
     fa = [np.frombuffer(f, dtype=np.uint8) for f in filters]
     fp = (C.c_void_p * len(fa))(*[a.ctypes.data for a in fa])
+    fpu = (u8p * len(fa))(*[_ptr(a) for a in fa])
     fl = np.array([a.size for a in fa], dtype=np.uint64)
     mask = np.zeros(max(nq, 1), dtype=np.uint8)
 
     def probe_part(r):
         lo, hi = nq * r // threads, nq * (r + 1) // threads
-        if hi > lo:
+        if hi <= lo:
+            return
+        if R is not None:
             R.ref_full_probe_many(fp, _ptr(fl, u64p), len(fa), q[lo * 20:].ctypes.data_as(C.c_char_p),
                                   hi - lo, 20, mask[lo:].ctypes.data)
+        else:
+            L.orc_full_probe_many(fpu, _ptr(fl, u64p), len(fa), _ptr(q[lo * 20:]), 20, hi - lo,
+                                  _ptr(mask[lo:]), 1)
 
+    nl = len(tables) if legacy_tables is None else legacy_tables
     with ThreadPoolExecutor(max_workers=threads) as ex:  # ctypes calls release the GIL
         t0 = time.perf_counter()
         built = list(ex.map(build_one, tables))
         t1 = time.perf_counter()
         list(ex.map(probe_part, range(threads)))
         t2 = time.perf_counter()
-    return t1 - t0, t2 - t1, built, mask[:nq]
+        leg = list(ex.map(legacy_one, tables[:nl]))
+        t3 = time.perf_counter()
+    return {"build_s": t1 - t0, "probe_s": t2 - t1, "legacy_s": t3 - t2, "legacy_tables": nl,
+            "built": built, "mask": mask[:nq], "legacy": leg}
 
 
 def ref_lib():

@@ -36,10 +36,19 @@ def golden():
 @pytest.fixture(scope="session")
 def gpu():
     """A dlsm_amd context on cuda:0 (GPU tests only)."""
+    import torch
+
     import dlsm_amd
 
     if not dlsm_amd.device_available():
         pytest.fail("GPU test requested but no HIP device is visible")
     ctx = dlsm_amd.Context(0)
+    # one stream for torch's tensor ops and the context: inputs a test makes
+    # with torch are ordered before the library's kernels that read them
+    s = torch.cuda.Stream(device=0)
+    torch.cuda.set_stream(s)
+    ctx.set_stream(s)
     yield ctx
+    torch.cuda.synchronize()
+    ctx.set_stream(None)
     ctx.close()

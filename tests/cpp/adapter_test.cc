@@ -116,6 +116,100 @@ int main() {
             (orc_legacy_key_may_match(want.data(), wl, reinterpret_cast<const uint8_t*>(q),
                                       std::strlen(q)) != 0));
   }
+  // ---- FilterPolicy surface through base-class pointers (Options::filter_policy):
+  // NewBloomFilterPolicy, and InternalFilterPolicy over internal keys, both the
+  // GPU form (suffix_len 8 on the device) and the generic wrapper form ----
+  {
+    const dlsm_adapter::FilterPolicy* user = dlsm_adapter::NewBloomFilterPolicy(10, ctx);
+    dlsm_adapter::BloomFilterPolicy gpu_user(10, ctx);
+    dlsm_adapter::InternalFilterPolicy ip_gpu(&gpu_user);
+    dlsm_adapter::InternalFilterPolicy ip_wrap(user);  // any FilterPolicy: host-side ExtractUserKey
+    const dlsm_adapter::FilterPolicy* policies[3] = {user, &ip_gpu, &ip_wrap};
+    const bool internal[3] = {false, true, true};
+    std::vector<std::string> uk;
+    for (int i = 0; i < 3000; i++) {
+      uint8_t k[20];
+      orc_dbbench_key(static_cast<uint64_t>(i) * 7 + 3, 20, k);
+      uk.emplace_back(reinterpret_cast<char*>(k), 20);
+    }
+    uk.push_back("");      // empty user key
+    uk.push_back("x");     // 1-byte tail (sign-extended bytes live in the fixtures)
+    std::string flat;
+    std::vector<uint64_t> offs{0};
+    for (auto& s : uk) {
+      flat += s;
+      offs.push_back(flat.size());
+    }
+    std::vector<uint8_t> want(8192, 0);
+    const int64_t wl = orc_legacy_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0,
+                                        uk.size(), 10, want.data(), want.size());
+    CHECK(wl > 0);
+    for (int p = 0; p < 3; p++) {
+      const dlsm_adapter::FilterPolicy* pol = policies[p];
+      CHECK(std::strcmp(pol->Name(), "TimberSaw.BuiltinBloomFilter2") == 0);
+      std::vector<std::string> ks;  // user keys, or internal keys user||Fixed64(seq<<8|type)
+      for (size_t i = 0; i < uk.size(); i++) {
+        std::string k = uk[i];
+        if (internal[p]) {
+          const uint64_t tag = (static_cast<uint64_t>(1000 + i) << 8) | 1u;
+          k.append(reinterpret_cast<const char*>(&tag), 8);  // little-endian host
+        }
+        ks.push_back(k);
+      }
+      std::vector<Slice> keys(ks.begin(), ks.end());
+      std::vector<char> buf(16 * 1024, 0);
+      Slice dst(buf.data(), 0);
+      dst.append("ab", 2);
+      pol->CreateFilter(keys.data(), static_cast<int>(keys.size()), &dst);
+      CHECK(static_cast<int64_t>(dst.size()) == 2 + wl);
+      CHECK(std::memcmp(dst.data() + 2, want.data(), wl) == 0);
+      if (internal[p])  // the reference rewrites keys[] to the user keys (dbformat.cc:97-101)
+        for (size_t i = 0; i < keys.size(); i++) CHECK(keys[i].size() == uk[i].size() && keys[i].data() == ks[i].data());
+      Slice filt(dst.data() + 2, wl);
+      for (size_t i = 0; i < ks.size(); i += 7) CHECK(pol->KeyMayMatch(Slice(ks[i]), filt));
+      for (int q = 0; q < 2000; q++) {
+        uint8_t k[28];
+        orc_dbbench_key(static_cast<uint64_t>(q) * 7 + 5, 20, k);  // mostly absent
+        const uint64_t tag = (static_cast<uint64_t>(q) << 8) | 1u;
+        std::memcpy(k + 20, &tag, 8);
+        const bool got = pol->KeyMayMatch(Slice(reinterpret_cast<char*>(k), internal[p] ? 28 : 20), filt);
+        CHECK(got == (orc_legacy_key_may_match(want.data(), wl, k, 20) != 0));
+      }
+    }
+    delete user;
+  }
+  // ---- FullFilterBlockBuilder: repeated user keys (several versions of a key
+  // in a compaction output) lower the line count; the builder asks for the
+  // exact count; keys of mixed length take the offsets path ----
+  {
+    std::vector<char> slot(256 * 1024, 0);
+    dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx);
+    for (int mixed = 0; mixed < 2; mixed++) {
+      std::string flat;
+      std::vector<uint64_t> offs{0};
+      b.RestartBlock(0);
+      for (int i = 0; i < 60000; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i / 3), 20, k);  // 3 versions per user key
+        const int len = mixed ? 12 + (i / 3) % 9 : 20;
+        b.AddKey(Slice(reinterpret_cast<char*>(k), len));
+        flat.append(reinterpret_cast<char*>(k), len);
+        offs.push_back(flat.size());
+      }
+      b.Finish();
+      CHECK(b.status() == DLSM_OK);
+      std::vector<uint8_t> want(256 * 1024, 0);
+      const int64_t wl = orc_full_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0, 60000, 10,
+                                        want.data(), want.size());
+      uint32_t L60k = 0;
+      uint64_t n60k = 0;
+      dlsm_bloom_full_size(60000, 10, &L60k, &n60k);
+      CHECK(wl > 0 && static_cast<uint64_t>(wl) < n60k && static_cast<int64_t>(b.result.size()) == wl);
+      CHECK(std::memcmp(b.result.data(), want.data(), wl) == 0);
+      b.Reset();
+    }
+  }
   // ---- FilterBlockBuilder / FilterBlockReader: TableBuilder's call shape
   // (StartBlock after each data block flush, filter_block.cc:32-38) ----
   {

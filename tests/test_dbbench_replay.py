@@ -1,5 +1,6 @@
-"""dbbench_replay.py (BASELINE config 5): the replayed flush filters and Get
-probes equal the oracle's on the same streams."""
+"""dbbench_replay.py (BASELINE config 5): every filter the replay builds --
+memtable flushes and leveled-compaction outputs -- and every Get's filter
+answers equal the oracle's on the same streams."""
 import numpy as np
 import pytest
 
@@ -19,18 +20,54 @@ def test_streams_match_oracle_generators():
     assert np.array_equal(reads[:, 3], oracle.mt_values(1000 + threads + 3 + 1, num * threads, num))
 
 
-@pytest.mark.gpu
-def test_replay_parity(gpu):
+def test_level_limits_follow_reference_constants():
     import dbbench_replay as R
 
-    res, (mem, filters, reads, masks) = R.run(20_000, 16, 10, reps=1)
-    assert res["flushes"] == len(mem) == 3
-    for v, f in zip(mem, filters):
+    assert R.max_bytes_for_level(1) == 256 * 1048576 and R.max_bytes_for_level(3) == 25600 * 1048576
+    # a 64 MiB SSTable (options.h:157) holds one memtable's worth of entries (db/memtable.h:7)
+    assert R.MAX_FILE_ENTRIES == R.MEMTABLE_ENTRIES
+    assert abs(R.MAX_FILE_ENTRIES * R.ENTRY_BYTES - 64 * 1048576) < 0.001 * 64 * 1048576
+
+
+def _files_for_oracle(files):
+    return [type("F", (), dict(level=f.level, number=f.number, smallest=f.smallest, largest=f.largest,
+                               largest_trailer=f.largest_trailer, filter=f.filter)) for f in files]
+
+
+@pytest.mark.gpu
+def test_replay_parity_with_compactions(gpu):
+    """640 K writes: 5 flushes, their L0 -> L1 compactions and L1 -> L2 spills
+    (level limits scaled down so every level is exercised)."""
+    import dbbench_replay as R
+
+    built = []
+
+    def on_build(values, filters):
+        built.extend(zip(values, filters))
+
+    reads_seen = []
+
+    def on_read(b0, vals, masks, files):
+        reads_seen.append((vals, masks, files))
+
+    saved = R.LEVEL_BASE_BYTES
+    R.LEVEL_BASE_BYTES = 2 * R.MAX_FILE_ENTRIES * R.ENTRY_BYTES  # L1 spills after 2 files
+    try:
+        res, lsm = R.run(40_000, 16, 10, on_build=on_build, on_read=on_read, read_batch=200_000)
+    finally:
+        R.LEVEL_BASE_BYTES = saved
+    assert res["flushes"] == 5 and res["fill"]["compactions"] >= 5
+    assert res["fill"]["compaction_builds"] > 5 and sum(res["version"]["files_per_level"][2:]) > 0
+    assert res["fill"]["flush_builds"] + res["fill"]["compaction_builds"] == len(built)
+    for v, f in built:  # every filter the replay built
         assert f == oracle.full_build(oracle.keys_from_values(v), v.size)
-    files = [type("F", (), dict(level=0, number=j + 1, smallest=oracle.keys_from_values(v[:1]).tobytes(),
-                                largest=oracle.keys_from_values(v[-1:]).tobytes(),
-                                largest_trailer=(1 << 8) | 1, filter=f))
-             for j, (v, f) in enumerate(zip(mem, filters))]
-    sample = slice(0, 50_000)
-    want, _ = oracle.version_probe(files, oracle.keys_from_values(reads[sample]), 50_000, (1 << 56) - 1)
-    assert np.array_equal(masks[sample], want)
+    # the final version holds every written key (a key may sit in several
+    # levels: an older version below a newer one), each level key-disjoint
+    allv = np.concatenate([f.values for lv in lsm.levels for f in lv])
+    assert np.array_equal(np.unique(allv), np.unique(R.fill_stream(40_000, 16)))
+    for lv in lsm.levels[1:]:
+        assert all(a.largest < b.smallest for a, b in zip(lv, lv[1:]))
+    for vals, masks, files in reads_seen[:2]:
+        want, _ = oracle.version_probe(_files_for_oracle(files), oracle.keys_from_values(vals), vals.size,
+                                       (1 << 56) - 1)
+        assert np.array_equal(masks, want)

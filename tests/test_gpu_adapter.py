@@ -1,5 +1,8 @@
 """The C++ adapter (include/dlsm_bloom_adapter.hpp) compiled as a reference-side
-caller would compile it, run on the GPU, checked against the oracle."""
+caller would compile it, run on the GPU, checked against the oracle: the
+single-thread class surface (adapter_test.cc) and the reference's concurrent
+call shape, 16 builder threads with one context each (concurrent_builders.cc)."""
+import json
 import os
 import subprocess
 
@@ -8,10 +11,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _compile(tmp_path):
-    exe = tmp_path / "adapter_test"
-    cmd = ["g++", "-std=c++17", "-O2", "-I", os.path.join(ROOT, "include"),
-           os.path.join(ROOT, "tests", "cpp", "adapter_test.cc"),
+def _compile(tmp_path, name, extra=()):
+    exe = tmp_path / name
+    cmd = ["g++", "-std=c++17", "-O2", "-fno-rtti", "-fno-exceptions", "-pthread",
+           "-I", os.path.join(ROOT, "include"), *extra,
+           os.path.join(ROOT, "tests", "cpp", name + ".cc"),
            "-L", os.path.join(ROOT, "dlsm_amd", "lib"), "-ldlsm_bloom",
            "-L", os.path.join(ROOT, "oracle"), "-loracle",
            "-Wl,-rpath," + os.path.join(ROOT, "dlsm_amd", "lib"),
@@ -22,12 +26,58 @@ def _compile(tmp_path):
 
 
 def test_adapter_compiles_without_hip_headers(tmp_path):
-    """A reference-side C++ caller needs only the C header (no HIP, no torch)."""
-    _compile(tmp_path)
+    """A reference-side C++ caller needs only the C header (no HIP, no torch),
+    and builds with the reference's -fno-rtti -fno-exceptions."""
+    _compile(tmp_path, "adapter_test")
+    _compile(tmp_path, "concurrent_builders")
+
+
+def test_adapter_derives_from_host_filter_policy(tmp_path):
+    """With DLSM_ADAPTER_HOST_NAMESPACE the adapter classes derive from the
+    host's own FilterPolicy and use its Slice (what Options::filter_policy
+    holds), checked here against a host namespace shaped like TimberSaw's."""
+    src = tmp_path / "host_ns.cc"
+    src.write_text(
+        "#include <cstddef>\n#include <cstring>\n#include <string>\n"
+        "namespace hostdb {\n"
+        "class Slice { public: Slice():d_(\"\"),n_(0){} Slice(const char* d,size_t n):d_(d),n_(n){}\n"
+        "  Slice(const std::string& s):d_(s.data()),n_(s.size()){}\n"
+        "  const char* data() const {return d_;} size_t size() const {return n_;}\n"
+        "  void Reset(const char* d,size_t n){d_=d;n_=n;} private: const char* d_; size_t n_; };\n"
+        "class FilterPolicy { public: virtual ~FilterPolicy() {}\n"
+        "  virtual const char* Name() const = 0;\n"
+        "  virtual void CreateFilter(const Slice* keys, int n, Slice* dst) const = 0;\n"
+        "  virtual bool KeyMayMatch(const Slice& key, const Slice& filter) const = 0; };\n"
+        "struct Options { const FilterPolicy* filter_policy = nullptr; };\n"
+        "}\n"
+        "#define DLSM_ADAPTER_HOST_NAMESPACE hostdb\n"
+        "#include \"dlsm_bloom_adapter.hpp\"\n"
+        "int main() { hostdb::Options o; o.filter_policy = dlsm_adapter::NewBloomFilterPolicy(10, nullptr);\n"
+        "  dlsm_adapter::InternalFilterPolicy ip(o.filter_policy); const hostdb::FilterPolicy* p = &ip;\n"
+        "  int r = std::strcmp(p->Name(), \"TimberSaw.BuiltinBloomFilter2\"); delete o.filter_policy; return r; }\n")
+    exe = tmp_path / "host_ns"
+    subprocess.run(["g++", "-std=c++17", "-fno-rtti", "-fno-exceptions", "-I", os.path.join(ROOT, "include"),
+                    str(src), "-L", os.path.join(ROOT, "dlsm_amd", "lib"), "-ldlsm_bloom",
+                    "-Wl,-rpath," + os.path.join(ROOT, "dlsm_amd", "lib"), "-Wl,-rpath,/opt/rocm/lib",
+                    "-L/opt/rocm/lib", "-o", str(exe)], check=True)
+    assert subprocess.run([str(exe)], timeout=60).returncode == 0
 
 
 @pytest.mark.gpu
 def test_adapter_on_gpu(tmp_path):
-    exe = _compile(tmp_path)
+    exe = _compile(tmp_path, "adapter_test")
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and "OK adapter" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+def test_sixteen_concurrent_builder_threads(tmp_path):
+    """16 std::threads, one dlsm_ctx each, RestartBlock / AddKey x 153,846 /
+    Finish per table: every filter equals the oracle's and no context
+    allocates device memory after its first table."""
+    exe = _compile(tmp_path, "concurrent_builders")
+    out = subprocess.run([str(exe), "16", "4", "153846"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0 and "OK concurrent builders" in out.stdout, out.stdout + out.stderr
+    rec = json.loads(out.stdout.splitlines()[0])
+    assert rec["failures"] == 0 and rec["no_device_alloc_after_warmup"]
+    print(json.dumps(rec))

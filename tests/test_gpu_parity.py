@@ -77,6 +77,7 @@ def test_full_build_dev_config4_batch(gpu, orc):
     for path in (1, 2):
         for o in outs:
             o.fill_(0xEE)  # garbage: the library must write every filter byte
+        torch.cuda.synchronize()  # torch's stream vs the context's own stream
         gpu.set_path(path)
         gpu.full_build_dev(tables, outs, lens, 10)
         gpu.sync()
@@ -335,6 +336,35 @@ def test_full_probe_many_filters_and_varlen(gpu, orc):
     got = gpu.full_probe(fs, dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]),
                                            len(keys), 0, offs))
     assert np.array_equal(got, want)
+
+
+def test_full_probe_sixteen_mixed_filters_k20(gpu, orc):
+    """The filter set Version::Get walks: 10 level-0 flushes (153,846 keys) +
+    6 level files of other sizes (up to 6.15 M keys, a 7.7 MB filter): 2 mask
+    bytes, 20-byte keys, every path, run twice (deterministic)."""
+    import torch
+
+    import dlsm_amd
+
+    sizes = [153_846] * 10 + [600_000, 1_600_000, 3_000_000, 615_384, 6_153_840, 2_000_000]
+    F = len(sizes)
+    filters = [orc.full_build(orc.dbbench_keys(f, F, n), n) for f, n in enumerate(sizes)]
+    nq = 2_000_003
+    q = orc.keys_from_values(orc.mt_values(4242, 2 * F * max(sizes), nq))
+    want = orc.full_probe(filters, q, nq, nthreads=8)
+    fs = gpu.filterset(filters)
+    qd = torch.from_numpy(q).cuda()
+    mask = torch.empty(2 * nq, dtype=torch.uint8, device="cuda")
+    for path in (0, 1, 0):
+        mask.fill_(0xEE)
+        gpu.set_path(path)
+        try:
+            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, 20), mask)
+            gpu.sync()
+        finally:
+            gpu.set_path(0)
+        assert np.array_equal(mask.cpu().numpy(), want), path
+    fs.close()
 
 
 def test_full_probe_log2_zero_branch(gpu, orc):
