@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--path", type=int, default=0, help="0 auto, 1 direct, 2 sliced")
     ap.add_argument("--probe-round", type=int, default=None,
                     help="keys per pipelined probe round (0 = one round, the default)")
+    ap.add_argument("--probe-serial", action="store_true",
+                    help="probe rounds one after another on one stream (with --probe-round)")
     ap.add_argument("--build-groups", type=int, default=0, help="pipelined build job groups (0/1 = one group)")
     ap.add_argument("--probe-chunk-lg", type=int, default=13,
                     help="log2 keys per probe partition chunk (12..14; library default 13)")
@@ -109,6 +111,8 @@ def main():
     ctx.set_path(args.path)
     if args.probe_round is not None:
         ctx.set_probe_round(args.probe_round)
+    if args.probe_serial:
+        ctx.set_probe_serial(True)
     ctx.set_build_groups(args.build_groups)
     ctx.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
     stream = torch.cuda.Stream(device=dev)
@@ -191,7 +195,8 @@ def main():
             "lookups": Q, "filters": F, "parallelism": par,
             "rank0_tables": work.tables, "rank0_lookups": qk.n,
             "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
-            "probe_round_keys": args.probe_round, "build_groups": args.build_groups,
+            "probe_round_keys": args.probe_round, "probe_serial": args.probe_serial,
+            "build_groups": args.build_groups,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {

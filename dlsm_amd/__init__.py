@@ -34,7 +34,7 @@ PATH_AUTO, PATH_DIRECT, PATH_SLICED = 0, 1, 2
 INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbformat.h:374-377)
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
-OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT = 3, 4, 5
+OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
 
 
 def lib():
@@ -248,6 +248,10 @@ class Context:
     def set_probe_round(self, keys: int):
         """Keys per pipelined probe round (0 = one round)."""
         self.set_option(OPT_PROBE_ROUND_KEYS, keys)
+
+    def set_probe_serial(self, serial: bool):
+        """Probe rounds one after another on this context's stream (DLSM_OPT_PROBE_ROUND_SERIAL)."""
+        self.set_option(OPT_PROBE_ROUND_SERIAL, 1 if serial else 0)
 
     def set_build_groups(self, groups: int):
         """Job groups of a pipelined build (0 = auto, 1..4)."""

@@ -96,6 +96,7 @@ struct dlsm_ctx {
   int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14; 13 = two 4,096-key units, 512 threads)
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
+  bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -113,6 +114,7 @@ struct dlsm_ctx {
   DevBuf<LegacyJobDev> ljobs;
   DevBuf<uint64_t> lstarts;
   // probe workspace
+  DevBuf<uint32_t> hashes;  // grouped probe: one BloomHash per lookup
   DevBuf<uint16_t> pos;
   DevBuf<uint8_t> smask;
   // host-API staging
@@ -134,16 +136,29 @@ struct dlsm_ctx {
   uint64_t host_cap = 0;
 };
 
+// A stacked image of the filters of one mask byte that share a line count
+// and probe count (at most 8): filter f answers in bit f % 8 of byte f / 8.
+struct ProbeGroup {
+  uint64_t* stacked = nullptr;  // L*64 u64 words
+  uint32_t L = 0, magic = 0;
+  int k = 0;
+  int mask_byte = 0;
+  bool first_of_byte = false;  // writes its mask byte; later groups of the byte OR into it
+};
+
 struct dlsm_filterset {
   int device = 0;
   int F = 0;
   uint8_t* blob = nullptr;
   uint64_t blob_bytes = 0;
   FilterDev* d_filters = nullptr;
+  FilterDev* d_slots = nullptr;  // 8 stacking slots per group
   std::vector<FilterDev> h;
-  uint64_t* stacked = nullptr;  // L*64 u64 words when stackable
-  uint32_t L = 0, magic = 0;
-  int k = 0;
+  // sliced probe: one group (<= 8 filters, one L and k: the bench's set) or
+  // several (filters of different sizes, > 8 filters); empty = direct only
+  // (a filter in the reference's log2_cache_line_size_ == 0 branch)
+  std::vector<ProbeGroup> groups;
+  uint64_t stacked_bytes = 0;
 };
 
 namespace {
@@ -343,6 +358,7 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (const char* v = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(v, nullptr, 10);
   if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
+  if (const char* v = getenv("DLSM_PROBE_SERIAL")) ctx->probe_serial = atoi(v) != 0;
   *out = ctx;
   return DLSM_OK;
 }
@@ -361,6 +377,7 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->ljobs.release();
   ctx->lstarts.release();
   ctx->pos.release();
+  ctx->hashes.release();
   ctx->smask.release();
   ctx->sel.release();
   ctx->st_keys.release();
@@ -430,6 +447,10 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > 2) return DLSM_E_ARG;
       ctx->build_exact = static_cast<int>(value);
       return DLSM_OK;
+    case DLSM_OPT_PROBE_ROUND_SERIAL:
+      if (value > 1) return DLSM_E_ARG;
+      ctx->probe_serial = value != 0;
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -444,7 +465,8 @@ int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   uint64_t pregion = 0;
   for (uint32_t C : {4096u, 8192u, 16384u})
     pregion = std::max<uint64_t>(pregion, ((max_keys + C - 1) / C) * probe_region(C));
-  DLSM_CHECK(ctx->entries.ensure(std::max(pkeys, pregion)));
+  const uint64_t bregion = ((max_keys + kBuildChunk - 1) / kBuildChunk + max_jobs) * kBuildRegion;
+  DLSM_CHECK(ctx->entries.ensure(std::max({pkeys, pregion, bregion})));
   DLSM_CHECK(ctx->pos.ensure(pkeys));
   DLSM_CHECK(ctx->smask.ensure(pregion));
   const uint64_t chunks = (max_keys + kBuildChunk - 1) / kBuildChunk + max_jobs;
@@ -464,7 +486,7 @@ int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_byte
     b += buf.cap * sizeof(*buf.p);
   };
   add(ctx->entries); add(ctx->tab); add(ctx->jobs); add(ctx->starts); add(ctx->dchunk);
-  add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->pos); add(ctx->smask);
+  add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->pos); add(ctx->smask); add(ctx->hashes);
   add(ctx->st_keys); add(ctx->st_offs); add(ctx->st_out); add(ctx->st_len); add(ctx->st_filter);
   add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_outp); add(ctx->crc_cap);
   add(ctx->crc_val); add(ctx->sel);
@@ -580,7 +602,10 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     d.reserved = 0;
     starts[j] = chunk;
     starts[n_jobs + j] = slice;
-    entry += (b.keys.n + 15) & ~uint64_t(15);  // 16-element aligned: 16-byte stores
+    // chunk regions of kBuildRegion entries (padded buckets), or the keys
+    // back to back, 16-element aligned: 16-byte stores
+    entry += DLSM_BUILD_UNITS ? static_cast<uint64_t>(d.n_chunks) * kBuildRegion
+                              : (b.keys.n + 15) & ~uint64_t(15);
     chunk += d.n_chunks;
     slice += d.n_slices;
     tabw += static_cast<uint64_t>(d.n_slices + 1) * d.n_chunks;
@@ -977,18 +1002,53 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
   if (e == hipSuccess)
     e = hipMemcpyAsync(fs->d_filters, h.data(), sizeof(FilterDev) * n_filters, hipMemcpyHostToDevice, s);
   fs->h = h;
-  // Stackable: <= 8 filters, common line count and probe count, 64-byte lines.
-  bool stack = n_filters <= 8;
-  for (int f = 0; f < n_filters && stack; f++)
-    stack = h[f].lg == 6 && h[f].L == h[0].L && h[f].k == h[0].k;
-  if (e == hipSuccess && stack) {
-    fs->L = h[0].L;
-    fs->magic = h[0].magic;
-    fs->k = h[0].k;
-    e = hipMalloc(reinterpret_cast<void**>(&fs->stacked), static_cast<uint64_t>(fs->L) * 512u);
-    if (e == hipSuccess) e = launch_stack_filters(fs->d_filters, n_filters, fs->L, fs->stacked, s);
+  // Sliced-probe groups: within each mask byte, the filters with one (L, k)
+  // share a stacked image.  Every filter must have 64-byte lines (the
+  // reader's common case) for the sliced path; otherwise the set is probed
+  // directly.
+  bool stack = true;
+  for (int f = 0; f < n_filters; f++) stack = stack && h[f].lg == 6;
+  std::vector<std::vector<int>> members;
+  if (stack) {
+    for (int b = 0; b * 8 < n_filters; b++) {
+      bool first = true;
+      std::vector<bool> done(8, false);
+      for (int f = 8 * b; f < std::min(n_filters, 8 * b + 8); f++) {
+        if (done[f - 8 * b]) continue;
+        ProbeGroup g;
+        g.L = h[f].L;
+        g.magic = h[f].magic;
+        g.k = h[f].k;
+        g.mask_byte = b;
+        g.first_of_byte = first;
+        first = false;
+        std::vector<int> m;
+        for (int q = f; q < std::min(n_filters, 8 * b + 8); q++)
+          if (!done[q - 8 * b] && h[q].L == g.L && h[q].k == g.k) {
+            done[q - 8 * b] = true;
+            m.push_back(q);
+          }
+        fs->groups.push_back(g);
+        members.push_back(m);
+      }
+    }
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  const size_t G = fs->groups.size();
+  if (e == hipSuccess && G) {
+    std::vector<FilterDev> slots(8 * G, FilterDev{nullptr, 0, 0, 0, 0});
+    for (size_t g = 0; g < G; g++)
+      for (int f : members[g]) slots[8 * g + (f % 8)] = h[f];
+    e = hipMalloc(reinterpret_cast<void**>(&fs->d_slots), sizeof(FilterDev) * slots.size());
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(fs->d_slots, slots.data(), sizeof(FilterDev) * slots.size(), hipMemcpyHostToDevice, s);
+    for (size_t g = 0; g < G && e == hipSuccess; g++) {
+      const uint64_t bytes = static_cast<uint64_t>(fs->groups[g].L) * 512u;
+      e = hipMalloc(reinterpret_cast<void**>(&fs->groups[g].stacked), bytes);
+      if (e == hipSuccess) e = launch_stack_filters(fs->d_slots + 8 * g, fs->groups[g].L, fs->groups[g].stacked, s);
+      fs->stacked_bytes += bytes;
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // `slots` is pageable host memory
   if (e != hipSuccess) {
     dlsm_filterset_destroy(fs);
     return from_hip(e);
@@ -1000,7 +1060,9 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
 int dlsm_filterset_destroy(dlsm_filterset* fs) {
   if (!fs) return DLSM_OK;
   DeviceGuard g(fs->device);
-  if (fs->stacked) (void)hipFree(fs->stacked);
+  for (auto& grp : fs->groups)
+    if (grp.stacked) (void)hipFree(grp.stacked);
+  if (fs->d_slots) (void)hipFree(fs->d_slots);
   if (fs->d_filters) (void)hipFree(fs->d_filters);
   if (fs->blob) (void)hipFree(fs->blob);
   delete fs;
@@ -1010,10 +1072,89 @@ int dlsm_filterset_destroy(dlsm_filterset* fs) {
 int dlsm_filterset_size(const dlsm_filterset* fs, int* n_filters, uint64_t* device_bytes) {
   if (!fs) return DLSM_E_ARG;
   if (n_filters) *n_filters = fs->F;
-  if (device_bytes)
-    *device_bytes = fs->blob_bytes + (fs->stacked ? static_cast<uint64_t>(fs->L) * 512u : 0);
+  if (device_bytes) *device_bytes = fs->blob_bytes + fs->stacked_bytes;
   return DLSM_OK;
 }
+
+namespace {
+
+// Slices of 2^lgR stacked lines for a group of line count L (a table with
+// more than kMaxSlices slices of 64 KiB moves to 128 KiB slices, one
+// workgroup per CU); 0 when the group cannot be sliced.
+uint32_t group_slices(const dlsm_ctx* ctx, uint32_t L, int* lgR) {
+  *lgR = ctx->probe_lgr;
+  uint32_t S = ceil_div_u32(L, 1u << *lgR);
+  if (S > kMaxSlices && *lgR < 8) {
+    *lgR = 8;
+    S = ceil_div_u32(L, 1u << *lgR);
+  }
+  return S >= 1 && S <= kMaxSlices ? S : 0;
+}
+
+// (slice, part) workgroups of the slice pass: about one resident wave of
+// workgroups (256 CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at
+// least one chunk per wave (a part's waves split its chunks into equal
+// groups).  ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU.)
+int slice_parts(uint32_t S, uint32_t nC, int lgR) {
+  static const uint32_t per_cu_env = [] {
+    const char* e = getenv("DLSM_SLICE_WGS_PER_CU");
+    return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+  }();
+  const uint32_t resident = 256u * (per_cu_env ? per_cu_env : (lgR == 7 ? 2u : 1u));
+  int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
+  return std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 16)));
+}
+
+// A filter set of several groups (filters of different sizes, more than 8
+// filters): every lookup is hashed ONCE (hash pass, 4 B per key), then each
+// group partitions the hashes by its own line count and probes its stacked
+// image, OR-ing its answer bits into the group's mask byte.  A group too large
+// to slice is probed directly from the same hashes.
+int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, int mode, uint8_t* mask_dev) {
+  hipStream_t s = ctx->stream;
+  const uint64_t n = kd.n;
+  const int lgC = ctx->probe_lgc;
+  const uint64_t C = 1ull << lgC;
+  const int mb = (fs->F + 7) / 8;
+  const uint32_t nC = ceil_div_u32(n, C);
+  DLSM_CHECK(ctx->hashes.ensure(n));
+  DLSM_TRY(launch_probe_hash(kd, ctx->hashes.p, mode, s));
+  KeyDesc hk{};
+  hk.bytes = reinterpret_cast<const uint8_t*>(ctx->hashes.p);
+  hk.offsets = nullptr;
+  hk.n = n;
+  hk.key_len = 4;
+  hk.suffix = 0;
+  uint32_t Smax = 0;
+  for (const auto& g : fs->groups) {
+    int lg;
+    Smax = std::max(Smax, group_slices(ctx, g.L, &lg));
+  }
+  const uint64_t rstride = static_cast<uint64_t>(nC) * probe_region(static_cast<uint32_t>(C));
+  DLSM_CHECK(ctx->entries.ensure(rstride));
+  DLSM_CHECK(ctx->pos.ensure(static_cast<uint64_t>(nC) * C));
+  DLSM_CHECK(ctx->smask.ensure(rstride));
+  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(Smax + 1) * nC));
+  for (size_t gi = 0; gi < fs->groups.size(); gi++) {
+    const ProbeGroup& g = fs->groups[gi];
+    int lgR;
+    const uint32_t S = group_slices(ctx, g.L, &lgR);
+    if (S == 0 || ctx->path == 1) {
+      DLSM_TRY(launch_probe_direct_group(fs->d_slots + 8 * gi, hk, mask_dev, mb, g.mask_byte,
+                                         g.first_of_byte, s));
+      continue;
+    }
+    DLSM_TRY(launch_probe_partition(hk, g.L, g.magic, lgR, S, ctx->entries.p, ctx->pos.p, ctx->tab.p,
+                                    KM_HASH, lgC, s));
+    DLSM_TRY(launch_probe_slices(g.stacked, g.L, g.magic, g.k, lgR, S, nC, ctx->entries.p, ctx->tab.p,
+                                 ctx->smask.p, slice_parts(S, nC, lgR), lgC, s));
+    DLSM_TRY(launch_probe_unpermute_group(n, ctx->pos.p, ctx->smask.p, mask_dev, mb, g.mask_byte,
+                                          g.first_of_byte, lgC, s));
+  }
+  return DLSM_OK;
+}
+
+}  // namespace
 
 int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
                               uint8_t* mask_dev) {
@@ -1026,34 +1167,39 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   hipStream_t s = ctx->stream;
   const int mode = is_k20(*keys) ? KM_K20 : (is_k28(*keys) ? KM_K28 : KM_GENERIC);
   const KeyDesc kd = to_desc(*keys);
-  // Slices of 2^lgR stacked lines; a table with more than kMaxSlices slices
-  // of 64 KiB moves to 128 KiB slices (one workgroup per CU).
-  int lgR = ctx->probe_lgr;
-  uint32_t S = fs->stacked ? ceil_div_u32(fs->L, 1u << lgR) : 0;
-  if (S > kMaxSlices && lgR < 8) {
-    lgR = 8;
-    S = ceil_div_u32(fs->L, 1u << lgR);
-  }
   const int lgC = ctx->probe_lgc;
   const uint64_t C = 1ull << lgC;
-  const bool sliced = ctx->path != 1 && fs->stacked && S >= 1 && S <= kMaxSlices &&
-                      keys->n <= 0xffffffffull * C;
-  if (ctx->path == 2 && !sliced) return DLSM_E_ARG;
-  if (!sliced) {
+  const bool fits = keys->n <= 0xffffffffull * C;
+  // The set's sliceable groups (all of them must be, for the forced sliced path).
+  bool all_sliceable = !fs->groups.empty();
+  for (const auto& grp : fs->groups) {
+    int lg;
+    all_sliceable = all_sliceable && group_slices(ctx, grp.L, &lg) != 0;
+  }
+  if (ctx->path == 2 && !(all_sliceable && fits)) return DLSM_E_ARG;
+  if (fs->groups.empty() || ctx->path == 1 || !fits) {
     DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
     return DLSM_OK;
   }
+  if (fs->groups.size() > 1 || !all_sliceable) return probe_grouped(ctx, fs, kd, mode, mask_dev);
+
+  // One group (the bench's set: <= 8 filters of one line count): the keys are
+  // hashed inside the partition pass.
+  const ProbeGroup& grp = fs->groups[0];
+  int lgR;
+  const uint32_t S = group_slices(ctx, grp.L, &lgR);
   // Rounds of probe_round keys, pipelined: round r's partition (helper
-  // stream) overlaps round r-1's slice + unpermute (context stream).  A
-  // round's intermediates (4 B hash + 2 B position + 1 B answer per key) live
-  // in one of kProbeBufs rotating buffers, small enough to stay resident in
-  // the 256 MiB Infinity Cache while the keys stream past.
+  // stream) overlaps round r-1's slice + unpermute (context stream), or
+  // serial (DLSM_OPT_PROBE_ROUND_SERIAL).  A round's intermediates (4 B hash +
+  // 2 B position + 1 B answer per key) live in one of kProbeBufs rotating
+  // buffers, small enough to stay resident in the 256 MiB Infinity Cache
+  // while the keys stream past.
   const uint64_t n = keys->n;
   uint64_t round = n;
   if (ctx->probe_round && ctx->probe_round < n)
     round = std::max<uint64_t>(C, (ctx->probe_round / C) * C);
   const uint64_t n_rounds = (n + round - 1) / round;
-  const bool pipe = n_rounds > 1;
+  const bool pipe = n_rounds > 1 && !ctx->probe_serial;
   const int nbuf = pipe ? kProbeBufs : 1;
   const uint32_t nCmax = ceil_div_u32(std::min(round, n), C);
   const uint64_t kstride = static_cast<uint64_t>(nCmax) * C;  // keys per buffer (16-B aligned)
@@ -1078,22 +1224,11 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     kr.n = nr;
     if (kd.offsets) kr.offsets = kd.offsets + r0;
     else kr.bytes = kd.bytes + r0 * kd.key_len;
-    // (slice, part) workgroups: about one resident wave of workgroups (256
-    // CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at least one
-    // chunk per wave (a part's waves split its chunks into equal groups).
-    // ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU: a tuning knob
-    // for the pipelined rounds, where a partition workgroup shares each CU)
-    static const uint32_t per_cu_env = [] {
-      const char* e = getenv("DLSM_SLICE_WGS_PER_CU");
-      return e ? static_cast<uint32_t>(atoi(e)) : 0u;
-    }();
-    const uint32_t resident = 256u * (per_cu_env ? per_cu_env : (lgR == 7 ? 2u : 1u));
-    int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
-    parts = std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 16)));
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
-    DLSM_TRY(launch_probe_partition(kr, fs->L, fs->magic, lgR, S, ent, pos, tab, mode, lgC, ps));
+    DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, lgR, S, ent, pos, tab, mode, lgC, ps));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
-    DLSM_TRY(launch_probe_slices(fs->stacked, fs->L, fs->magic, fs->k, lgR, S, nC, ent, tab, sm, parts, lgC, s));
+    DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, S, nC, ent, tab, sm,
+                                 slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }

@@ -15,7 +15,9 @@ namespace dlsm {
 // K20: packed 20-B user keys; K28: packed 28-B internal keys hashed as
 // ExtractUserKey (suffix 8) -- both 16-B-aligned fixed stride, LDS-tiled in
 // the partition passes (other kernels take the K28 keys on the generic path)
-enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1, KM_K28 = 2 };
+// KM_HASH: the "keys" are BloomHash values already (u32 each, from the hash
+// pass of a grouped probe): the partition loads them instead of hashing.
+enum KeyMode : int { KM_GENERIC = 0, KM_K20 = 1, KM_K28 = 2, KM_HASH = 3 };
 
 struct KeyDesc {
   const uint8_t* bytes;
@@ -87,6 +89,14 @@ constexpr uint32_t kBuildSliceCUs = 256;  // MI355X CUs: the build's slice-count
 #define DLSM_BUILD_CHUNK 4096
 #endif
 constexpr int kBuildChunk = DLSM_BUILD_CHUNK;  // keys per partition chunk (build)
+// DLSM_BUILD_UNITS: the build partition pads every slice bucket of a chunk to
+// whole 16-byte units (pad entries have bit 31 set), so the slice pass loads
+// 4 entries per lane per load; each chunk then owns a region of kBuildRegion
+// entries (its keys plus up to 3 pads per bucket).
+#ifndef DLSM_BUILD_UNITS
+#define DLSM_BUILD_UNITS 1  // r02: build slice 65.7 -> 50.8 us, build 0.176 -> 0.165 ms (profiles/r02_ab_units_pred.txt)
+#endif
+constexpr uint32_t kBuildRegion = DLSM_BUILD_UNITS ? kBuildChunk + 4u * kMaxSlices : kBuildChunk;
 constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
 // u32 entries (and answer bytes) per probe chunk region: C keys plus up to 3
 // padding entries per slice bucket (buckets are padded to 16-byte units).
@@ -115,8 +125,24 @@ hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, i
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
                                int mode, hipStream_t s);
-hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, uint64_t* stacked,
-                                hipStream_t s);
+// Direct probe of one group's 8 slots from precomputed hashes (KM_HASH keys):
+// the answer bits OR-ed (or, for the byte's first group, written) into byte
+// `byte` of each key's `stride`-byte mask entry.
+hipError_t launch_probe_direct_group(const FilterDev* slots, KeyDesc hashes, uint8_t* mask, int stride,
+                                     int byte, bool first, hipStream_t s);
+// Stacked image of up to 8 filters of one line count: slots[b] (b < 8) is the
+// filter whose answer goes to bit b of the answer byte, or has data == nullptr
+// (bit b stays 0).
+hipError_t launch_stack_filters(const FilterDev* slots, uint32_t L, uint64_t* stacked, hipStream_t s);
+// BloomHash of every key (u32 per key, coalesced): the grouped probe hashes
+// each lookup once and partitions the hashes once per filter group.
+hipError_t launch_probe_hash(KeyDesc keys, uint32_t* hashes, int mode, hipStream_t s);
+// Unpermute for a filter group of a multi-byte or multi-group set: answer
+// byte of key i to mask[i * stride + byte], OR-ed into what is there unless
+// `first` (the first group of that mask byte).
+hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
+                                        uint8_t* mask, int stride, int byte, bool first, int lgC,
+                                        hipStream_t s);
 // lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice (7, 8).
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,

@@ -80,6 +80,8 @@ __device__ __forceinline__ uint32_t key_hash(const KeyDesc& kd, uint64_t i) {
     return hash_k20(kd.bytes + i * 20u);
   } else if constexpr (MODE == KM_K28) {
     return hash_k20(kd.bytes + i * 28u);  // ExtractUserKey: the first 20 of 28 bytes
+  } else if constexpr (MODE == KM_HASH) {
+    return reinterpret_cast<const uint32_t*>(kd.bytes)[i];
   } else {
     uint64_t s, l;
     if (kd.offsets) {
@@ -360,6 +362,13 @@ __device__ __forceinline__ void hash_chunk(const KeyDesc& kd, uint64_t first, ui
       }
       __syncthreads();
     }
+  } else if constexpr (MODE == KM_HASH) {
+    const uint32_t* hp = reinterpret_cast<const uint32_t*>(kd.bytes) + first;
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + t;
+      h[r] = i < nk ? __builtin_nontemporal_load(hp + i) : 0u;  // coalesced dwords
+    }
   } else {
 #pragma unroll
     for (int r = 0; r < PER; r++) {
@@ -624,22 +633,21 @@ __device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds
 // partition).  One 512-thread workgroup per chunk of kBuildChunk keys of one
 // job.
 // ---------------------------------------------------------------------------
-// Build entries (DLSM_BUILD_LINE_IN_ENTRY): AddHash reads only hash bits
+// Build entries: AddHash reads only hash bits
 // [0, 9) and [17, 26) (bitpos = h & 511 stepping by rotr(h, 17), positions
 // mod 512, util/bloom_impl.h:427-443), so the partition parks the key's line
 // offset inside its slice (< 2^11) in bits [9, 17) and [26, 29): the slice
 // pass needs no modulo.  The full hash is gone, so the rare slice fallback
 // (duplicates lowered L) re-hashes the keys.
+// Bit 31 is never read either: real entries clear it, bucket padding sets it.
+[[maybe_unused]] constexpr uint32_t kBuildPadEntry = 0x80000000u;
 __device__ __forceinline__ uint32_t build_entry(uint32_t h, uint32_t off) {
-  return (h & 0xE3FE01FFu) | ((off & 0xffu) << 9) | ((off >> 8) << 26);
+  return (h & 0x63FE01FFu) | ((off & 0xffu) << 9) | ((off >> 8) << 26);
 }
 __device__ __forceinline__ uint32_t build_entry_off(uint32_t e) {
   return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
 }
 
-#ifndef DLSM_BUILD_LINE_IN_ENTRY
-#define DLSM_BUILD_LINE_IN_ENTRY 1
-#endif
 constexpr int kPartBlock = kBuildChunk / 8;  // 8 keys per thread (512 threads at 4,096-key chunks)
 
 // Job-wide distinct count (defined below; used by the exact partition).
@@ -660,9 +668,13 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   // key tile (K20), then the staging area of the bucketed hashes (both modes)
   constexpr int KB = mode_kb<MODE>();
   constexpr int TKV = K20Tile<kPartBlock, tile_kpt<KB>(), KB>::kVec;
-  constexpr int TVB = TKV > C / 4 ? TKV : C / 4;  // the staging area needs C u32
+  constexpr int RV = static_cast<int>(kBuildRegion) / 4;  // the staging area holds a (padded) chunk
+  constexpr int TVB = TKV > RV ? TKV : RV;
   __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
   __shared__ uint32_t hist[kMaxSlices + 1];
+#if DLSM_BUILD_UNITS
+  __shared__ uint8_t npad[kMaxSlices + 1];
+#endif
   __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
   __shared__ uint32_t wsum[kPartBlock / 64];
   __shared__ int sj;
@@ -704,23 +716,42 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
       const uint32_t line = fastmod(h[r], L, magic);
       const uint32_t s = line >> lgR;
       code[r] = (atomicAdd(&hist[s], 1u) << 9) | s;
-#if DLSM_BUILD_LINE_IN_ENTRY
       h[r] = build_entry(h[r], line & ((1u << lgR) - 1u));
-#endif
     }
   }
   __syncthreads();
-  block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
+#if DLSM_BUILD_UNITS
+  for (uint32_t b = tid; b < S; b += kPartBlock) {  // pad every bucket to whole 16-byte units
+    const uint32_t pad = (0u - hist[b]) & 3u;
+    npad[b] = static_cast<uint8_t>(pad);
+    hist[b] += pad;
+  }
+  __syncthreads();
+#endif
+  const uint32_t total = block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
   for (uint32_t b = tid; b <= S; b += kPartBlock)
     tab[J.tab0 + static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);  // free since hash_chunk's last barrier
+#if DLSM_BUILD_UNITS
+  for (uint32_t b = tid; b < S; b += kPartBlock) {
+    const uint32_t end = hist[b + 1], np = npad[b];
+    if (np > 0) stage[end - 1] = kBuildPadEntry;
+    if (np > 1) stage[end - 2] = kBuildPadEntry;
+    if (np > 2) stage[end - 3] = kBuildPadEntry;
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) stage[hist[code[r] & 511u] + (code[r] >> 9)] = h[r];
   }
   __syncthreads();
+#if DLSM_BUILD_UNITS
+  store_chunk_u32<kPartBlock>(entries + J.entry0 + static_cast<uint64_t>(c) * kBuildRegion, stage, total);
+#else
+  (void)total;
   store_chunk_u32<kPartBlock>(entries + J.entry0 + first, stage, nk);
+#endif
 }
 
 // Sum of a job's per-chunk distinct counts (every thread gets the total).
@@ -777,7 +808,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
     const uint16_t* __restrict__ tab, uint32_t block0) {
   constexpr uint32_t R = 1u << LGR;
-  constexpr int U = kWalkU;
+  [[maybe_unused]] constexpr int U = kWalkU;
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
@@ -810,10 +841,34 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       // (a job of >= 256 chunks keeps whole 64-chunk groups: measured 2 %
       // faster at 391 chunks than 8 groups of 49, gpurun_out v19b)
       const uint32_t gs = nC >= 256u ? 64u : max(1u, (nC + NW - 1) / NW);
+#if DLSM_BUILD_UNITS
+      // 16-byte units of 4 entries per lane per load (padding entries skipped)
+      constexpr int U4 = kWalkU / 4;
+      walk_segments<U4, kBuildRegion / 4, uint4>(
+          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
+          [&](const uint4 (&hv)[U4], const uint32_t (&)[U4], const bool (&ok)[U4], uint32_t) {
+            if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
+#pragma unroll
+              for (int u = 0; u < U4; u++) {
+                const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                  if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash_k<6>(sl + build_entry_off(e4[j]) * 16u, e4[j]);
+              }
+            } else {
+#pragma unroll
+              for (int u = 0; u < U4; u++) {
+                const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                  if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash(sl + build_entry_off(e4[j]) * 16u, e4[j], k);
+              }
+            }
+          });
+#else
       walk_segments<U, kBuildChunk>(
           tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
           [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
-#if DLSM_BUILD_LINE_IN_ENTRY
             if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
 #pragma unroll
               for (int u = 0; u < U; u++)
@@ -823,29 +878,14 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
               for (int u = 0; u < U; u++)
                 if (ok[u]) lds_add_hash(sl + build_entry_off(hv[u]) * 16u, hv[u], k);
             }
-#else
-            if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
-#pragma unroll
-              for (int u = 0; u < U; u++)
-                if (ok[u]) lds_add_hash_k<6>(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u]);
-            } else {
-#pragma unroll
-              for (int u = 0; u < U; u++)
-                if (ok[u]) lds_add_hash(sl + (fastmod(hv[u], L, magic) - lo_line) * 16u, hv[u], k);
-            }
-#endif
           });
+#endif
     } else {
       // Duplicates lowered the line count below the speculative one: the
-      // partition used the wrong modulus, so scan every hash of the job.
-#if DLSM_BUILD_LINE_IN_ENTRY
+      // partition used the wrong modulus (and the entries no longer hold the
+      // full hash), so re-hash every key of the job.
       for (uint64_t e = tid; e < J.keys.n; e += kSliceBlock) {
         const uint32_t hv = key_hash<KM_GENERIC>(J.keys, e);
-#else
-      const uint32_t* ent = entries + J.entry0;
-      for (uint64_t e = tid; e < J.keys.n; e += kSliceBlock) {
-        const uint32_t hv = ent[e];
-#endif
         const uint32_t line = fastmod(hv, L, magic);
         if ((line >> LGR) == s) lds_add_hash(sl + (line - lo_line) * 16u, hv, J.k);
       }
@@ -971,13 +1011,18 @@ __global__ __launch_bounds__(kBlock) void probe_direct_kernel(const FilterDev* _
 // `line` of filter f in its bit f, so one 1-byte LDS read answers a probe for
 // all 8 filters and ANDing the k bytes gives the key's answer byte directly.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* __restrict__ fs,
-                                                               int F, uint64_t words,
+__global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* __restrict__ slots,
+                                                               uint64_t words,
                                                                uint64_t* __restrict__ stacked) {
+  __shared__ const uint8_t* src[8];
+  if (threadIdx.x < 8) src[threadIdx.x] = slots[threadIdx.x].data;
+  __syncthreads();
   for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; w < words;
        w += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    uint64_t x = 0;  // byte f = byte w of filter f
-    for (int f = 0; f < F; f++) x |= static_cast<uint64_t>(fs[f].data[w]) << (8 * f);
+    uint64_t x = 0;  // byte b = byte w of the filter in slot b (0 for an empty slot)
+#pragma unroll
+    for (int f = 0; f < 8; f++)
+      if (src[f]) x |= static_cast<uint64_t>(src[f][w]) << (8 * f);
     // 8x8 bit transpose: bit b of byte f -> bit f of byte b
     uint64_t t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
     x ^= t ^ (t << 7);
@@ -1009,7 +1054,9 @@ __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
 // grouped by slice, every bucket padded to a multiple of 4 entries with
 // kProbePadEntry, so the slice pass moves whole 16-byte units; pos[i] = where
 // key i went.  NT threads per chunk of C keys (C/NT keys per thread).
-template <int MODE, int NT, int C, int H = 1>
+// NTS: non-temporal stores of the intermediates (default); plain stores
+// leave them in the Infinity Cache for a round-sized batch to re-read.
+template <int MODE, int NT, int C, int H = 1, bool NTS = true>
 __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
@@ -1049,7 +1096,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   // software-pipelined across units and chunks (hash_chunk_k20_pipe) -- one
   // resident workgroup per CU would otherwise leave its CU's HBM stream idle
   // during the bucket / scan / scatter / store phases.
-  constexpr bool kPipe = MODE != KM_GENERIC && PER <= 8 && PER / KPT >= 2;
+  constexpr bool kPipe = (MODE == KM_K20 || MODE == KM_K28) && PER <= 8 && PER / KPT >= 2;
   uint4 pre[2][TL::kPer];
   if constexpr (kPipe) {
     if (blockIdx.x < nC) {
@@ -1129,8 +1176,8 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     }
     __syncthreads();
     // coalesced 16-byte stores of the bucketed entries and of the positions
-    store_chunk_u32<NT, true>(entries + static_cast<uint64_t>(c) * CR, stage, total);
-    store_chunk_u16<NT, true>(pos + first, rk, nk);
+    store_chunk_u32<NT, NTS>(entries + static_cast<uint64_t>(c) * CR, stage, total);
+    store_chunk_u16<NT, NTS>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
   }
 }
@@ -1508,10 +1555,69 @@ hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys,
   return hipGetLastError();
 }
 
-hipError_t launch_stack_filters(const FilterDev* fs, int n_filters, uint32_t L, uint64_t* stacked,
-                                hipStream_t s) {
+__global__ __launch_bounds__(kBlock) void probe_direct_group_kernel(const FilterDev* __restrict__ slots,
+                                                                    KeyDesc hk, uint8_t* __restrict__ mask,
+                                                                    int stride, int byte, int first) {
+  __shared__ FilterDev sf[8];
+  if (threadIdx.x < 8) sf[threadIdx.x] = slots[threadIdx.x];
+  __syncthreads();
+  const uint32_t* hv = reinterpret_cast<const uint32_t*>(hk.bytes);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; i < hk.n;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint32_t h = hv[i];
+    uint32_t m = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++)
+      if (sf[b].data) m |= full_may_match(h, sf[b]) << b;
+    uint8_t* o = mask + i * static_cast<uint64_t>(stride) + byte;
+    *o = first ? static_cast<uint8_t>(m) : static_cast<uint8_t>(*o | m);
+  }
+}
+
+hipError_t launch_probe_direct_group(const FilterDev* slots, KeyDesc hashes, uint8_t* mask, int stride,
+                                     int byte, bool first, hipStream_t s) {
+  if (hashes.n == 0) return hipSuccess;
+  probe_direct_group_kernel<<<grid_for(hashes.n, 256u * 64u), kBlock, 0, s>>>(slots, hashes, mask, stride,
+                                                                              byte, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_stack_filters(const FilterDev* slots, uint32_t L, uint64_t* stacked, hipStream_t s) {
   const uint64_t words = static_cast<uint64_t>(L) * 64u;
-  stack_filters_kernel<<<grid_for(words), kBlock, 0, s>>>(fs, n_filters, words, stacked);
+  stack_filters_kernel<<<grid_for(words), kBlock, 0, s>>>(slots, words, stacked);
+  return hipGetLastError();
+}
+
+// Hash pass of the grouped probe: one 512-thread workgroup per 4,096 keys,
+// the key tiles staged through LDS like the partition's (K20 / K28), the
+// hashes stored coalesced.
+template <int MODE>
+__global__ __launch_bounds__(512) void probe_hash_kernel(KeyDesc kd, uint32_t* __restrict__ hashes) {
+  constexpr int NT = 512, C = 4096, PER = C / NT;
+  constexpr int KB = mode_kb<MODE>();
+  constexpr int TV = K20Tile<NT, tile_kpt<KB>(), KB>::kVec;
+  __shared__ __attribute__((aligned(16))) uint4 tile[TV];
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * C;
+  const uint64_t left = kd.n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+  uint32_t h[PER];
+  hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const uint32_t i = r * NT + threadIdx.x;
+    if (i < nk) hashes[first + i] = h[r];
+  }
+}
+
+hipError_t launch_probe_hash(KeyDesc keys, uint32_t* hashes, int mode, hipStream_t s) {
+  if (keys.n == 0) return hipSuccess;
+  const unsigned g = static_cast<unsigned>((keys.n + 4095) / 4096);
+  if (mode == KM_K20)
+    probe_hash_kernel<KM_K20><<<g, 512, 0, s>>>(keys, hashes);
+  else if (mode == KM_K28)
+    probe_hash_kernel<KM_K28><<<g, 512, 0, s>>>(keys, hashes);
+  else
+    probe_hash_kernel<KM_GENERIC><<<g, 512, 0, s>>>(keys, hashes);
   return hipGetLastError();
 }
 
@@ -1552,7 +1658,19 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
     return e ? static_cast<uint32_t>(atoi(e)) : 2u;
   }();
   const uint32_t g = per_cu ? std::min(nC, per_cu * device_cus()) : nC;
-  if (mode == KM_K20)
+  // $DLSM_PROBE_PLAIN_STORES=1: plain (Infinity-Cache-allocating) intermediate
+  // stores, for round-sized batches (A/B knob; K20 keys only)
+  static const bool plain = [] {
+    const char* e = getenv("DLSM_PROBE_PLAIN_STORES");
+    return e && atoi(e) != 0;
+  }();
+  if (mode == KM_HASH)
+    probe_partition_kernel<KM_HASH, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+                                                           entries, pos, tab);
+  else if (mode == KM_K20 && plain)
+    probe_partition_kernel<KM_K20, NT, C, H, false><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+                                                                 entries, pos, tab);
+  else if (mode == KM_K20)
     probe_partition_kernel<KM_K20, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
                                                           entries, pos, tab);
   else if (mode == KM_K28)
@@ -1631,6 +1749,44 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
     default: return hipErrorInvalidValue;
   }
 #undef DLSM_UNPERMUTE
+  return hipGetLastError();
+}
+
+// Grouped-probe unpermute: like probe_unpermute_kernel, but the answer byte
+// goes to byte `byte` of the key's `stride`-byte mask entry, OR-ed into it
+// unless this is the first group of that byte.
+template <int C>
+__global__ __launch_bounds__(kBlock) void probe_unpermute_group_kernel(
+    uint64_t n, const uint16_t* __restrict__ pos, const uint8_t* __restrict__ smask,
+    uint8_t* __restrict__ mask, int stride, int byte, int first_group) {
+  constexpr uint32_t CR = probe_region(C);
+  __shared__ __attribute__((aligned(16))) uint8_t sm[CR];
+  const int tid = threadIdx.x;
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * C;
+  const uint64_t left = n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+  const uint32_t nvec = (min(CR, nk + 4u * kMaxSlices) + 15u) / 16u;
+  const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(blockIdx.x) * CR);
+  for (uint32_t v = tid; v < nvec; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
+  __syncthreads();
+  for (uint32_t i = tid; i < nk; i += kBlock) {
+    uint8_t* o = mask + (first + i) * static_cast<uint64_t>(stride) + byte;
+    const uint8_t a = sm[pos[first + i]];
+    *o = first_group ? a : static_cast<uint8_t>(*o | a);
+  }
+}
+
+hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
+                                        uint8_t* mask, int stride, int byte, bool first, int lgC,
+                                        hipStream_t s) {
+  if (n_keys == 0) return hipSuccess;
+  const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
+  switch (lgC) {
+    case 12: probe_unpermute_group_kernel<4096><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
+    case 13: probe_unpermute_group_kernel<8192><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
+    case 14: probe_unpermute_group_kernel<16384><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

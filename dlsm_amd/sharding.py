@@ -130,6 +130,9 @@ def make_inputs(ctx, work: RankWork, keys_per_table: int, n_filters: int, bits_p
     from . import workload as W
 
     N, F, bpk = keys_per_table, n_filters, bits_per_key
+    # torch makes the inputs on `stream` (or its current stream); every library
+    # call below starts after a device synchronise, so nothing depends on the
+    # context using the same stream
     ctxm = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
     with ctxm:
         tables, outs = [], []
@@ -149,6 +152,7 @@ def make_inputs(ctx, work: RankWork, keys_per_table: int, n_filters: int, bits_p
                 v = torch.arange(N, device=dev, dtype=torch.int64) * step + first
                 ftabs.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), N, 20))
             flens = torch.zeros(F, dtype=torch.uint64, device=dev)
+        torch.cuda.synchronize(dev)
         ctx.full_build_dev(ftabs, fouts, flens, bpk)
         ctx.sync()
         assert all(int(x) == flen for x in flens.cpu().numpy())
@@ -162,12 +166,13 @@ def make_inputs(ctx, work: RankWork, keys_per_table: int, n_filters: int, bits_p
                 h = fouts[f].cpu()
                 dist.broadcast(h, src=0)
                 fouts[f].copy_(h.to(dev))
-        torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(dev)
     fs = ctx.filterset(fouts, on_device=True)
     qv = lookup_values(work, 2 * F * N)
     with ctxm:
         q = W.dbbench_keys_torch(torch.from_numpy(qv.astype(np.int64)).to(dev))
         mask = torch.empty(max(1, work.n_lookups) * fs.mask_bytes, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
     return RankInputs(tables, outs, lens, fouts, fs, dlsm_amd.Keys(q, work.n_lookups, 20), mask)
 
 

@@ -142,13 +142,17 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             internal keys (suffix_len > 0) or per-key lengths (offsets),
  *                             whose duplicate user keys lower the line count; 1 always;
  *                             2 never (one pass; a batch whose duplicates change the line
- *                             count then takes a slower per-slice re-hash fallback) */
+ *                             count then takes a slower per-slice re-hash fallback)
+ *   DLSM_OPT_PROBE_ROUND_SERIAL 1: probe rounds run one after another on the context
+ *                             stream (one buffer set) instead of pipelined over two
+ *                             streams (default 0, or $DLSM_PROBE_SERIAL) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
 #define DLSM_OPT_PROBE_CHUNK_LG 3
 #define DLSM_OPT_PROBE_SLICE_LG 4
 #define DLSM_OPT_BUILD_EXACT 5
+#define DLSM_OPT_PROBE_ROUND_SERIAL 6
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 
 /* Page-lock a host range (e.g. an RDMA-registered FilterChunk slot) so D2H

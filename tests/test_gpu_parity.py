@@ -367,6 +367,47 @@ def test_full_probe_sixteen_mixed_filters_k20(gpu, orc):
     fs.close()
 
 
+@pytest.mark.parametrize("shape", ["mixed8", "equal16", "mixed11_k28"])
+def test_full_probe_grouped_sliced(gpu, orc, shape):
+    """Filter sets of several (L, k) groups take the grouped sliced probe (one
+    hash pass, one partition + slice + unpermute per group, OR-ed mask bytes):
+    filters of different sizes, 16 equal filters (two mask bytes), 11 filters
+    of 3 sizes probed with 28-byte internal keys.  Forced sliced and auto
+    against direct and the oracle."""
+    import torch
+
+    import dlsm_amd
+
+    sizes = {"mixed8": [153_846, 153_846, 600_000, 600_000, 1_600_000, 1_600_000, 3_000_000, 3_000_000],
+             "equal16": [200_000] * 16,
+             "mixed11_k28": [50_000, 90_000, 50_000, 120_000, 90_000, 50_000, 50_000, 120_000, 90_000,
+                             50_000, 120_000]}[shape]
+    F = len(sizes)
+    filters = [orc.full_build(orc.dbbench_keys(f, F, n), n) for f, n in enumerate(sizes)]
+    nq = 1_500_007
+    q = orc.keys_from_values(orc.mt_values(17, 2 * F * max(sizes), nq))
+    want = orc.full_probe(filters, q, nq, nthreads=8)
+    klen = 20
+    if shape.endswith("k28"):
+        trl = np.random.default_rng(3).integers(0, 256, size=(nq, 8), dtype=np.uint8)
+        q = np.ascontiguousarray(np.hstack([q.reshape(nq, 20), trl]).reshape(-1))
+        klen = 28
+    fs = gpu.filterset(filters)
+    mb = (F + 7) // 8
+    qd = torch.from_numpy(q).cuda()
+    mask = torch.empty(mb * nq, dtype=torch.uint8, device="cuda")
+    for path in (2, 0, 1):
+        mask.fill_(0xEE)
+        gpu.set_path(path)
+        try:
+            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, nq, klen, suffix_len=klen - 20), mask)
+            gpu.sync()
+        finally:
+            gpu.set_path(0)
+        assert np.array_equal(mask.cpu().numpy(), want), (shape, path)
+    fs.close()
+
+
 def test_full_probe_log2_zero_branch(gpu, orc):
     """A filter whose num_lines*64 != len but len % num_lines == 0: the reference
     probes it with log2_cache_line_size_ == 0 (full_filter_block.h:85)."""

@@ -26,6 +26,27 @@ def _free_port():
     return p
 
 
+def _collect(procs, q, timeout):
+    """rank 0's result from the queue; fails as soon as a rank dies instead
+    of waiting out the timeout."""
+    import queue
+    import time
+
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        try:
+            return q.get(timeout=2)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead:
+                for p in procs:
+                    p.kill()
+                raise AssertionError(f"a rank exited with {dead}")
+    for p in procs:
+        p.kill()
+    raise AssertionError("ranks timed out")
+
+
 def _cpu_worker(rank, world, port, q):
     import torch.distributed as dist
 
@@ -59,7 +80,7 @@ def test_two_rank_gloo_strong_plan():
     procs = [ctx.Process(target=_cpu_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    t, gathered = q.get(timeout=300)
+    t, gathered = _collect(procs, q, 300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -118,11 +139,14 @@ def _gpu_worker(rank, world, port, q):
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     ctx = dlsm_amd.Context(0)
+    stream = torch.cuda.Stream(device=dev)  # as bench.py: torch and the context share it
+    ctx.set_stream(stream)
     work = SH.plan(rank, world, _T, _N, _Q, "strong")
-    inp = SH.make_inputs(ctx, work, _N, _F, 10, dev, dist=dist)
+    inp = SH.make_inputs(ctx, work, _N, _F, 10, dev, stream=stream, dist=dist)
     for _ in range(2):  # the bench's step, twice (the second reuses the job table)
         SH.step(ctx, inp, 10)
     ctx.sync()
+    torch.cuda.synchronize()
     L = inp.lens.cpu().numpy()
     filters = {s: inp.outs[j][: int(L[j])].cpu().numpy().tobytes() for j, s in enumerate(work.tables)}
     out = (work.tables, filters, inp.mask[: work.n_lookups].cpu().numpy().tobytes(),
@@ -145,7 +169,7 @@ def test_two_ranks_on_gpu_strong_scaling_parity(orc):
     procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    gathered = q.get(timeout=600)
+    gathered = _collect(procs, q, 240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
