@@ -511,7 +511,7 @@ struct SegWalk {
   // next group starts instead of being waited on where it is issued.
   __device__ __forceinline__ uint32_t load_rows(uint32_t gg) const {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t c = min(gg + lane, g_end - 1u);  // clamped: unconditional loads
+    const uint32_t c = min(min(gg, g_end) + lane, g_end - 1u);  // clamped: unconditional loads
     const uint16_t* r = tb + static_cast<uint64_t>(c) * rowlen;
     return static_cast<uint32_t>(r[0]) | (static_cast<uint32_t>(r[1]) << 16);
   }
@@ -526,11 +526,15 @@ struct SegWalk {
     nz = uniform64(__ballot(cnt != 0u));
     e0 = 0;
   }
+  // The next group's rows are prefetched unconditionally (load_rows clamps
+  // past-the-end groups to the last chunk): a prefetch under a branch makes
+  // the compiler merge the two values of nrow with a copy that waits
+  // (s_waitcnt vmcnt(0)) right after the load is issued.
   __device__ __forceinline__ bool start(uint32_t g_first) {
     g = g_first;
     if (g >= g_end) return false;
     const uint32_t row = load_rows(g);
-    if (g + g_step < g_end) nrow = load_rows(g + g_step);
+    nrow = load_rows(g + g_step);
     setup(row);
     return true;
   }
@@ -540,7 +544,7 @@ struct SegWalk {
       g += g_step;
       if (g >= g_end) return false;
       const uint32_t row = nrow;
-      if (g + g_step < g_end) nrow = load_rows(g + g_step);
+      nrow = load_rows(g + g_step);
       setup(row);
     }
     seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
@@ -1049,6 +1053,42 @@ __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
   return (h & ~(kEntryLineMask | kProbePadEntry)) | (line_off << 9);
 }
 
+// Phase timestamps of the persistent probe partition (diagnostic builds only,
+// make variant TAG=stamps VFLAGS=-DDLSM_STAMPS=1; scripts/partition_stamps.py):
+// wave 0 of workgroup b stamps s_memtime at the phase ends of its chunk
+// iteration it.
+#if DLSM_STAMPS
+constexpr int kStampWGs = 1024, kStampIters = 64, kStampPhases = 8;
+__device__ uint64_t g_stamps[kStampWGs * kStampIters * kStampPhases];
+#define DLSM_STAMP(ph, it)                                                                     \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < kStampWGs && (it) < kStampIters)                      \
+      g_stamps[(blockIdx.x * kStampIters + (it)) * kStampPhases + (ph)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define DLSM_STAMP(ph, it) \
+  do {                     \
+  } while (0)
+#endif
+
+// s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 simm16:
+// vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]).
+constexpr int kWaitVmcnt0 = 0x0F70;
+
+// f(b) for every bucket b < n (n <= kMaxSlices + 1): one bucket per thread
+// when the workgroup has enough threads.  A strided loop's per-lane trip
+// count is a loop invariant the persistent partition spilled to scratch, and
+// every scratch reload is an s_waitcnt vmcnt(0) that drained the key tiles
+// in flight once per chunk.
+template <int NT, typename F>
+__device__ __forceinline__ void for_buckets(uint32_t n, F f) {
+  if constexpr (NT > kMaxSlices) {
+    if (threadIdx.x < n) f(threadIdx.x);
+  } else {
+    for (uint32_t b = threadIdx.x; b < n; b += NT) f(b);
+  }
+}
+
 // Pass 1: hash each lookup once and bucket it by slice inside its chunk.
 // entries[chunk region of probe_region(C) u32] = packed entries (probe_entry)
 // grouped by slice, every bucket padded to a multiple of 4 entries with
@@ -1108,9 +1148,11 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   }
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
   for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
+    [[maybe_unused]] const uint32_t it = (c - blockIdx.x) / gridDim.x;
+    DLSM_STAMP(0, it);
     const uint64_t first = static_cast<uint64_t>(c) * C;
     const uint32_t nk = chunk_keys(c);
-    for (uint32_t b = tid; b <= S; b += NT) hist[b] = 0;
+    for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
     uint32_t h[PER];
 #pragma unroll
     for (int u = 0; u < H; u++) {
@@ -1124,6 +1166,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
       } else {
         hash_chunk<MODE, NT, PER>(kd, fu, nku, tile, h);  // ends with a barrier
       }
+      DLSM_STAMP(1 + 2 * (u & 1), it);
 #pragma unroll
       for (int r = 0; r < PER; r++) {
         const uint32_t il = r * NT + tid;
@@ -1137,24 +1180,27 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
           if (u + 1 < H) park[i] = h[r];
         }
       }
+      DLSM_STAMP(2 + 2 * (u & 1), it);
     }
     __syncthreads();
-    for (uint32_t b = tid; b < S; b += NT) {  // pad every bucket to whole 16-byte units
+    for_buckets<NT>(S, [&](uint32_t b) {  // pad every bucket to whole 16-byte units
       const uint32_t pad = (0u - hist[b]) & 3u;
       npad[b] = static_cast<uint8_t>(pad);
       hist[b] += pad;
-    }
+    });
     __syncthreads();
     const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
-    for (uint32_t b = tid; b <= S; b += NT)
-      tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);  // one row per chunk
-    for (uint32_t b = tid; b < S; b += NT) {
+    DLSM_STAMP(5, it);
+    for_buckets<NT>(S + 1, [&](uint32_t b) {  // one row per chunk
+      tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
+    });
+    for_buckets<NT>(S, [&](uint32_t b) {
       const uint32_t end = hist[b + 1];
       const uint32_t np = npad[b];
       if (np > 0) stage[end - 1] = kProbePadEntry;
       if (np > 1) stage[end - 2] = kProbePadEntry;
       if (np > 2) stage[end - 3] = kProbePadEntry;
-    }
+    });
     const uint32_t nkl = unit_keys(nk, H - 1);
 #pragma unroll
     for (int r = 0; r < PER; r++) {  // the last unit, from registers
@@ -1175,10 +1221,16 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
       }
     }
     __syncthreads();
+    DLSM_STAMP(6, it);
+    // The next unit's key tiles (issued before the bucketing) are waited for
+    // HERE, while only loads are in flight: once the stores below are pending
+    // every wait is a full vmcnt(0) that would also wait for their acks.
+    if constexpr (kPipe) __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     // coalesced 16-byte stores of the bucketed entries and of the positions
     store_chunk_u32<NT, NTS>(entries + static_cast<uint64_t>(c) * CR, stage, total);
     store_chunk_u16<NT, NTS>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
+    DLSM_STAMP(7, it);
   }
 }
 
@@ -1205,7 +1257,10 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t lo_line = s << LGR;
   const uint32_t nl = min(R, L - lo_line);
   {
-    // all of the slice's 16-byte loads in flight before the first LDS store
+    // all of the slice's 16-byte loads in flight before the first LDS store.
+    // Loads AND stores are clamped (lanes past the slice rewrite its last
+    // unit with the same bytes): a store under a branch let the compiler sink
+    // each load into its branch, one HBM round trip per load.
     constexpr int V = R * 32 / NT;
     const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 512u);
     uint4* dst = reinterpret_cast<uint4*>(sl);
@@ -1214,8 +1269,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
 #pragma unroll
     for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
 #pragma unroll
-    for (int v = 0; v < V; v++)
-      if (static_cast<uint32_t>(v * NT + tid) < nw) dst[v * NT + tid] = t[v];
+    for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
   }
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
@@ -1887,3 +1941,12 @@ hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t ma
 }
 
 }  // namespace dlsm
+
+#if DLSM_STAMPS
+// Diagnostic builds only: copy the partition's phase stamps to the host.
+extern "C" int dlsm_debug_stamps(uint64_t* host, uint64_t n) {
+  const uint64_t cap = static_cast<uint64_t>(dlsm::kStampWGs) * dlsm::kStampIters * dlsm::kStampPhases;
+  if (n > cap) n = cap;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dlsm::g_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif

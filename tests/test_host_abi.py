@@ -107,3 +107,27 @@ def test_host_crc32c_helper(orc, golden):
     for c in golden["full"]["crc32c"]:
         assert dlsm_amd.crc32c(bytes.fromhex(c["data"])) == c["crc"]
     assert dlsm_amd.crc32c_mask(dlsm_amd.crc32c(b"foo")) == orc.crc32c_mask(orc.crc32c(b"foo"))
+
+
+def test_slice_kernels_use_no_scratch(tmp_path):
+    """No slice kernel spills to scratch.  The sliced-probe corruption of
+    commit 1c7c4c6 needed a scratch spill (a forced 64-VGPR bound) together
+    with two 1,024-thread workgroups per CU (tests/diag/run_old_slice.py);
+    keeping the slice passes spill-free rules that combination out."""
+    src = os.path.join(ROOT, "dlsm_amd", "csrc", "bloom_kernels.hip")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950",
+                        "--offload-device-only", "-c", src, "-o", str(tmp_path / "k.o"),
+                        "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    usage, name = {}, None
+    for line in r.stderr.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+        m = re.search(r"remark:\s+ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and name:
+            usage[name] = int(m.group(1))
+    slices = {k: v for k, v in usage.items() if "slice_kernel" in k}
+    assert len(slices) >= 6, sorted(usage)
+    assert all(v == 0 for v in slices.values()), slices
