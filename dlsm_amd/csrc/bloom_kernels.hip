@@ -197,6 +197,21 @@ __device__ __forceinline__ void lds_add_hash_k(uint32_t* line, uint32_t h) {
   }
 }
 
+#if DLSM_ABL_BUILD_NOCF
+// Ablation (timing only, wrong filters): the same k LDS ORs with lane l's
+// words all in bank l & 31 -- the build slice pass without bank conflicts.
+template <int K>
+__device__ __forceinline__ void lds_add_hash_nocf(uint32_t* sl, uint32_t h) {
+  const uint32_t delta = bloom_delta(h);
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    const uint32_t bp = h & 511u;
+    atomicOr(&sl[((bp >> 5) << 5) | (threadIdx.x & 31u)], 1u << (bp & 31u));
+    h += delta;
+  }
+}
+#endif
+
 // Filter trailer (full_filter_block.cc:133-135): k byte + Fixed32 num_lines.
 __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
   uint8_t* t = out + static_cast<uint64_t>(L) * 64u;
@@ -554,8 +569,17 @@ struct SegWalk {
   }
   __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
     const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
+#if DLSM_ABL_NOLOAD  // ablation (timing only, wrong answers): the walk without its entry loads
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if constexpr (sizeof(E) == 16) hv[u] = make_uint4(idx[u] * 0x9e3779b9u, idx[u], idx[u] << 7, idx[u] ^ gset);
+      else hv[u] = idx[u] * 0x9e3779b9u;
+    }
+    (void)gent;
+#else
 #pragma unroll
     for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
+#endif
   }
 };
 
@@ -857,7 +881,11 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
                 const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
 #pragma unroll
                 for (int j = 0; j < 4; j++)
+#if DLSM_ABL_BUILD_NOCF
+                  if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash_nocf<6>(sl, e4[j]);
+#else
                   if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash_k<6>(sl + build_entry_off(e4[j]) * 16u, e4[j]);
+#endif
               }
             } else {
 #pragma unroll
@@ -1300,6 +1328,10 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
               for (int q = 0; q < K; q++) {
 #if DLSM_ABL_NOLDS  // ablation (timing only, wrong answers): no LDS probe reads
                 acc &= (base | (x & 511u)) >> 3;
+#elif DLSM_ABL_NOCONFLICT  // ablation (timing only, wrong answers): lane l reads bank l & 31
+                acc &= sl[((x & 511u) << 8) | ((threadIdx.x & 31u) << 2)];
+#elif DLSM_ABL_TRANSPOSED  // ablation (timing only, wrong answers): [bitpos][line] address, random banks
+                acc &= sl[((x & 511u) << 8) | (base >> 9)];
 #else
                 acc &= sl[base | (x & 511u)];
 #endif
