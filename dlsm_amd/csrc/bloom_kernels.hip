@@ -495,6 +495,57 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
   }
 }
 
+// LDS-assisted form of seg_locate_win (DLSM_WALK_LDS, the default): no
+// per-boundary scalar loop.  At group setup the non-empty segments' dv are
+// compacted into the wave's LDS list dvc[0..); per window, every segment
+// that starts inside the window marks its start lane in the wave's 64-flag
+// array, one ballot of the flags gives the window's boundary mask B, and lane
+// j's segment is the (cw + popcount(B & lanes <= j))-th non-empty one, cw =
+// the count of segments started at or before the window start.  Cost per
+// window: 2 LDS writes + 2 LDS reads + 2 ballots + a few VALU, against a
+// dependent readlane / s_ff1 chain per boundary (ablation: the walk alone
+// took 87 of the slice pass's 177 us).  The arrays are wave-private and a
+// wave's LDS operations complete in order, so no barrier is needed; a
+// wavefront-scope fence between the flag stores and the flag load keeps the
+// compiler from treating the exchange as single-thread memory.  The pointers
+// carry the LDS address space (a generic pointer would become flat accesses).
+#ifndef DLSM_WALK_LDS
+#define DLSM_WALK_LDS 1
+#endif
+constexpr int kWalkScratch = 128;  // u32 per wave: 64 flags + 64 compacted dv
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <int U>
+__device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, uint32_t T, uint32_t w0,
+                                                   lds_u32* flg, const lds_u32* dvc,
+                                                   uint32_t (&idx)[U], bool (&ok)[U]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool live = (nz >> lane) & 1u;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t w = w0 + u * kWin;
+    if (w >= T) {  // wave-uniform
+      ok[u] = false;
+      idx[u] = lane;
+      continue;
+    }
+    const uint32_t cw = static_cast<uint32_t>(__builtin_popcountll(uniform64(__ballot(excl <= w) & nz)));
+    flg[lane] = 0u;
+    const uint32_t r = excl - w;
+    if (live && excl > w && r < kWin) flg[r] = 1u;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t f = flg[lane];
+    const uint64_t b = __ballot(f != 0u);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
+    const uint32_t d = dvc[cw + below + f - 1u];
+    const uint32_t id = w + lane + d;
+    const uint32_t id0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0));
+    ok[u] = w + lane < T;
+    idx[u] = ok[u] ? id : id0;
+  }
+}
+
 // One wave's walk over a slice's segments in the chunk groups g = g_first,
 // g_first + g_step, ... < g_end (gs <= 64 chunks per group, one per lane: a
 // caller with few chunks per wave shrinks gs so every wave of the workgroup
@@ -517,6 +568,7 @@ struct SegWalk {
   uint32_t gs;        // chunks per group (<= 64; lanes >= gs hold empty segments)
   uint32_t g;         // current group (first chunk)
   uint32_t e0;        // next window start in the current group
+  lds_u32* scr;       // the wave's kWalkScratch u32 of LDS (DLSM_WALK_LDS)
   uint32_t excl, dv, T;
   uint64_t nz;        // non-empty segments of the current group
   uint32_t nrow;      // prefetched table row pair of group g + g_step (this lane's chunk), packed
@@ -540,6 +592,13 @@ struct SegWalk {
     dv = lane * CHUNK + a0 - excl;
     nz = uniform64(__ballot(cnt != 0u));
     e0 = 0;
+#if DLSM_WALK_LDS
+    if (cnt != 0u) {  // compact the non-empty segments' dv (ordered by lane = by excl)
+      const uint32_t k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(nz >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(nz), 0u));
+      scr[64 + k] = dv;
+    }
+#endif
   }
   // The next group's rows are prefetched unconditionally (load_rows clamps
   // past-the-end groups to the last chunk): a prefetch under a branch makes
@@ -562,7 +621,11 @@ struct SegWalk {
       nrow = load_rows(g + g_step);
       setup(row);
     }
+#if DLSM_WALK_LDS
+    seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + 64, idx, ok);
+#else
     seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
+#endif
     e0 += kWin * U;
     gset = g;
     return true;
@@ -596,9 +659,10 @@ struct WinSet {
 template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, typename Act>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
-                                              Act act) {
+                                              uint32_t* scratch, Act act) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
   SegWalk<U, CHUNK, E> w{tb, entries, rowlen, g_step, g_end, gs};
+  w.scr = (lds_u32*)scratch;  // generic -> LDS address space (addrspacecast)
   if (!w.start(g_first)) return;
   WinSet<U, CHUNK, E> A, B;
   if (!w.next(A.idx, A.ok, A.g)) return;
@@ -840,6 +904,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
+  __shared__ uint32_t walk_scr[NW * kWalkScratch];
   __shared__ int sj;
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
@@ -873,7 +938,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       // 16-byte units of 4 entries per lane per load (padding entries skipped)
       constexpr int U4 = kWalkU / 4;
       walk_segments<U4, kBuildRegion / 4, uint4>(
-          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
+          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs, walk_scr + wv * kWalkScratch,
           [&](const uint4 (&hv)[U4], const uint32_t (&)[U4], const bool (&ok)[U4], uint32_t) {
             if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
 #pragma unroll
@@ -899,7 +964,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
           });
 #else
       walk_segments<U, kBuildChunk>(
-          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs,
+          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs, walk_scr + wv * kWalkScratch,
           [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
             if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
 #pragma unroll
@@ -1277,6 +1342,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   constexpr int U = LGR >= 8 ? kProbeWalkU8 : kProbeWalkU;
   constexpr int NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
+  __shared__ uint32_t walk_scr[NW * kWalkScratch];
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
@@ -1309,7 +1375,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // (the answers mirror the entries' layout).
   const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
   walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
-      tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs,
+      tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch,
       [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
         uint32_t ans[U];
