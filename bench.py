@@ -211,7 +211,9 @@ def main():
     }
     del rank_keys
 
-    traffic = load_traffic(args.traffic, result["config"], dominant)
+    # the committed PMC traffic is for the whole job on one GPU: a rank's
+    # share at N > 1 is not what was counted, so it is reported only at N = 1
+    traffic = load_traffic(args.traffic, result["config"], dominant) if world == 1 else None
     if traffic:
         result["roofline"]["traffic"] = traffic["traffic_bytes"]
         result["roofline"]["traffic_source"] = traffic["source"]
