@@ -212,6 +212,9 @@ bool is_k28(const dlsm_keyset& k) {
 // 8 KiB) while the batch has fewer than two slice workgroups per CU -- a
 // batch of dLSM-sized flush tables (153,846 keys, 3,005 lines) would
 // otherwise leave most CUs idle.  Returns -1 if none fits.
+#ifndef DLSM_BUILD_MIN_LGR
+#define DLSM_BUILD_MIN_LGR 9  // widest-first search starts at 2^9 lines (32 KiB slices)
+#endif
 int choose_build_lgR(const std::vector<uint32_t>& Ls) {
   auto slices = [&](int lg, uint64_t* total) {
     bool ok = true;
@@ -224,7 +227,7 @@ int choose_build_lgR(const std::vector<uint32_t>& Ls) {
     return ok;
   };
   uint64_t total = 0, t2 = 0;
-  for (int lg = 9; lg <= 11; lg++) {
+  for (int lg = DLSM_BUILD_MIN_LGR; lg <= 11; lg++) {
     if (!slices(lg, &total)) continue;
     while (lg > 7 && total < 2u * kBuildSliceCUs && slices(lg - 1, &t2)) {
       lg--;

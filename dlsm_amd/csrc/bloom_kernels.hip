@@ -1907,7 +1907,7 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
 // Grouped-probe unpermute: like probe_unpermute_kernel, but the answer byte
 // goes to byte `byte` of the key's `stride`-byte mask entry, OR-ed into it
 // unless this is the first group of that byte.
-template <int C>
+template <int C, int VEC>
 __global__ __launch_bounds__(kBlock) void probe_unpermute_group_kernel(
     uint64_t n, const uint16_t* __restrict__ pos, const uint8_t* __restrict__ smask,
     uint8_t* __restrict__ mask, int stride, int byte, int first_group) {
@@ -1921,10 +1921,73 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_group_kernel(
   const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(blockIdx.x) * CR);
   for (uint32_t v = tid; v < nvec; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
   __syncthreads();
-  for (uint32_t i = tid; i < nk; i += kBlock) {
-    uint8_t* o = mask + (first + i) * static_cast<uint64_t>(stride) + byte;
-    const uint8_t a = sm[pos[first + i]];
-    *o = first_group ? a : static_cast<uint8_t>(*o | a);
+  // 8 keys per thread: one 16-byte load of their positions; VEC = 1 (one
+  // mask byte per key) / 2 (two: 9..16 filters), mask aligned to 8 VEC bytes:
+  // one 8- / 16-byte read-modify-write of their mask bytes; VEC = 0: byte
+  // accesses at the group's byte of each key's stride.
+  for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
+    if (i0 + 8u <= nk) {
+      const uint4 pv = *reinterpret_cast<const uint4*>(pos + first + i0);
+      const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        lo |= uint32_t(sm[pw[q] & 0xffffu]) << (16 * q);
+        lo |= uint32_t(sm[pw[q] >> 16]) << (16 * q + 8);
+        hi |= uint32_t(sm[pw[q + 2] & 0xffffu]) << (16 * q);
+        hi |= uint32_t(sm[pw[q + 2] >> 16]) << (16 * q + 8);
+      }
+      if constexpr (VEC == 1) {
+        uint2* o = reinterpret_cast<uint2*>(mask + first + i0);
+        if (!first_group) {
+          const uint2 m = *o;
+          lo |= m.x;
+          hi |= m.y;
+        }
+        *o = make_uint2(lo, hi);
+      } else if constexpr (VEC == 2) {
+        // key b's two mask bytes are the 16-bit lane b; the group owns byte `byte` of each
+        uint4* o = reinterpret_cast<uint4*>(mask + (first + i0) * 2u);
+        const uint32_t sh = 8u * static_cast<uint32_t>(byte);
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const uint32_t src = q < 2 ? lo : hi;
+          const uint32_t a0 = (src >> (16 * (q & 1))) & 0xffu, a1 = (src >> (16 * (q & 1) + 8)) & 0xffu;
+          w[q] = (a0 << sh) | (a1 << (16u + sh));
+        }
+        uint4 m = make_uint4(w[0], w[1], w[2], w[3]);
+        if (!first_group) {
+          const uint4 old = *o;
+          m.x |= old.x;
+          m.y |= old.y;
+          m.z |= old.z;
+          m.w |= old.w;
+        } else {
+          // the first group of this byte writes it; keep the other byte
+          const uint4 old = *o;
+          const uint32_t keep = ~((0xffu << sh) | (0xffu << (16u + sh)));
+          m.x |= old.x & keep;
+          m.y |= old.y & keep;
+          m.z |= old.z & keep;
+          m.w |= old.w & keep;
+        }
+        *o = m;
+      } else {
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          uint8_t* o = mask + (first + i0 + b) * static_cast<uint64_t>(stride) + byte;
+          const uint8_t a = static_cast<uint8_t>((b < 4 ? lo : hi) >> (8 * (b & 3)));
+          *o = first_group ? a : static_cast<uint8_t>(*o | a);
+        }
+      }
+    } else {
+      for (uint32_t i = i0; i < nk; i++) {
+        uint8_t* o = mask + (first + i) * static_cast<uint64_t>(stride) + byte;
+        const uint8_t a = sm[pos[first + i]];
+        *o = first_group ? a : static_cast<uint8_t>(*o | a);
+      }
+    }
   }
 }
 
@@ -1933,12 +1996,19 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
                                         hipStream_t s) {
   if (n_keys == 0) return hipSuccess;
   const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(mask);
+  const int vec = (stride == 1 && (a & 7u) == 0) ? 1 : (stride == 2 && (a & 15u) == 0) ? 2 : 0;
+#define DLSM_UNPERM_G(CC)                                                                                       \
+  (vec == 1   ? (probe_unpermute_group_kernel<CC, 1><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first), 0) \
+   : vec == 2 ? (probe_unpermute_group_kernel<CC, 2><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first), 0) \
+              : (probe_unpermute_group_kernel<CC, 0><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first), 0))
   switch (lgC) {
-    case 12: probe_unpermute_group_kernel<4096><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
-    case 13: probe_unpermute_group_kernel<8192><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
-    case 14: probe_unpermute_group_kernel<16384><<<nC, kBlock, 0, s>>>(n_keys, pos, smask, mask, stride, byte, first); break;
+    case 12: DLSM_UNPERM_G(4096); break;
+    case 13: DLSM_UNPERM_G(8192); break;
+    case 14: DLSM_UNPERM_G(16384); break;
     default: return hipErrorInvalidValue;
   }
+#undef DLSM_UNPERM_G
   return hipGetLastError();
 }
 
