@@ -439,6 +439,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
 
 constexpr uint32_t kWin = 64;  // entries per walk window (one per lane)
 
+// s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 simm16:
+// vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]).
+constexpr int kWaitVmcnt0 = 0x0F70;
+
 // The wave's index in its workgroup as a wave-uniform (SGPR) value: derived
 // from threadIdx.x the compiler would treat it, and every walk counter built
 // from it, as divergent (exec-mask loops, vmcnt(0) waits on prefetches).
@@ -472,9 +476,9 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t w = w0 + u * kWin;
-    if (w >= T) {  // wave-uniform
+    if (w >= T) {  // wave-uniform; never for u = 0 (next() only runs with e0 < T)
       ok[u] = false;
-      idx[u] = lane;
+      idx[u] = u > 0 ? idx[0] : lane;  // re-reads window 0's units: see walk_segments
       continue;
     }
     const uint64_t below = uniform64(__ballot(excl <= w) & nz);
@@ -512,6 +516,12 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 #ifndef DLSM_WALK_LDS
 #define DLSM_WALK_LDS 1
 #endif
+#ifndef DLSM_WALK_PROLOGUE_WAIT
+#define DLSM_WALK_PROLOGUE_WAIT 1
+#endif
+#ifndef DLSM_PROBE_UNCOND_STORE
+#define DLSM_PROBE_UNCOND_STORE 1
+#endif
 constexpr int kWalkScratch = 128;  // u32 per wave: 64 flags + 64 compacted dv
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
@@ -524,9 +534,9 @@ __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, u
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t w = w0 + u * kWin;
-    if (w >= T) {  // wave-uniform
+    if (w >= T) {  // wave-uniform; never for u = 0 (next() only runs with e0 < T)
       ok[u] = false;
-      idx[u] = lane;
+      idx[u] = u > 0 ? idx[0] : lane;  // re-reads window 0's units: see walk_segments
       continue;
     }
     const uint32_t cw = static_cast<uint32_t>(__builtin_popcountll(uniform64(__ballot(excl <= w) & nz)));
@@ -614,12 +624,23 @@ struct SegWalk {
   }
   // Locate the next window set; false when the walk is done.
   __device__ __forceinline__ bool next(uint32_t (&idx)[U], bool (&ok)[U], uint32_t& gset) {
-    while (e0 >= T) {
+    if (e0 >= T) {
       g += g_step;
       if (g >= g_end) return false;
-      const uint32_t row = nrow;
-      nrow = load_rows(g + g_step);
-      setup(row);
+      setup(nrow);
+      nrow = load_rows(g + g_step);  // after setup: the load can refill nrow's register (no copy, no wait)
+      // Empty groups (rare): their successors' rows are loaded and waited
+      // on here.  Reusing the prefetched row in this loop would put a use of
+      // a just-issued load on one path into the group change, and the
+      // compiler's single wait for nrow there would be a vmcnt(0) on every
+      // path -- a drain of every load and store in flight once per group.
+      while (e0 >= T) {
+        g += g_step;
+        if (g >= g_end) return false;
+        const uint32_t row2 = load_rows(g);
+        nrow = load_rows(g + g_step);
+        setup(row2);
+      }
     }
 #if DLSM_WALK_LDS
     seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + 64, idx, ok);
@@ -667,6 +688,14 @@ __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowle
   WinSet<U, CHUNK, E> A, B;
   if (!w.next(A.idx, A.ok, A.g)) return;
   w.fetch(A.idx, A.g, A.hv);
+#if DLSM_WALK_PROLOGUE_WAIT
+  // The first set's loads land in A's registers, which the loop refills by
+  // copies: left pending into the loop, the compiler's wait for them merges
+  // with the loop's state into an s_waitcnt vmcnt(0) placed right after every
+  // iteration's prefetch -- each set's loads were waited on where they were
+  // issued.  Waiting once here keeps the loop's waits at the copies.
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+#endif
   bool haveB = false;
   if constexpr (DEPTH == 2) {
     haveB = w.next(B.idx, B.ok, B.g);
@@ -1164,10 +1193,6 @@ __device__ uint64_t g_stamps[kStampWGs * kStampIters * kStampPhases];
   } while (0)
 #endif
 
-// s_waitcnt vmcnt(0), expcnt and lgkmcnt left at their maxima (gfx9 simm16:
-// vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]).
-constexpr int kWaitVmcnt0 = 0x0F70;
-
 // f(b) for every bucket b < n (n <= kMaxSlices + 1): one bucket per thread
 // when the workgroup has enough threads.  A strided loop's per-lane trip
 // count is a loop invariant the persistent partition spilled to scratch, and
@@ -1413,10 +1438,18 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
           }
           ans[u] = a;
         }
+        // Stores are unconditional: a lane past the window's end holds the
+        // index (and so the entries and the answer) of a valid lane of the same
+        // set, so it rewrites that lane's dword with the same value.  A store
+        // under a branch makes the compiler's wait for the next set's loads a
+        // vmcnt(0) that also waits for these stores' acks (every path must
+        // agree on the count).
 #pragma unroll
         for (int u = 0; u < U; u++)
 #if DLSM_ABL_NOSTORE  // ablation (timing only): almost no answer stores
           if (ok[u] && ans[u] == 0x12345678u && (hv[u].x & 0xfff) == 0x123u) gmask[idx[u]] = ans[u];
+#elif DLSM_PROBE_UNCOND_STORE
+          gmask[idx[u]] = ans[u];
 #else
           if (ok[u]) gmask[idx[u]] = ans[u];
 #endif
