@@ -522,8 +522,14 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 #ifndef DLSM_PROBE_UNCOND_STORE
 #define DLSM_PROBE_UNCOND_STORE 1
 #endif
-constexpr int kWalkScratch = 128;  // u32 per wave: 64 flags + 64 compacted dv
+#ifndef DLSM_WALK_SET
+#define DLSM_WALK_SET 1
+#endif
+constexpr int kWalkScratch = 192;  // u32 per wave: 64 x min(U, 2) flags + 64 compacted dv
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// flags per wave for a walk of U windows per set (seg_locate_set_lds for U <= 2)
+template <int U>
+constexpr int walk_flags() { return (DLSM_WALK_SET && U <= 2) ? 64 * U : 64; }
 
 template <int U>
 __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, uint32_t T, uint32_t w0,
@@ -556,6 +562,46 @@ __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, u
   }
 }
 
+// Set-wide form (DLSM_WALK_SET, U <= 2): the flags of the whole window set
+// are marked at once and stamped with the set's tag instead of being cleared
+// (a wave-private running count, the array initialised to ~0 at the walk's
+// start), so a set costs one flag store, one fence, then per window one flag
+// read + one list read, and the windows' chains are independent.  A segment
+// starting exactly at window u's start is counted in cw, so lane 0's flag is
+// ignored.
+template <int U>
+__device__ __forceinline__ void seg_locate_set_lds(uint32_t excl, uint64_t nz, uint32_t T, uint32_t w0,
+                                                   uint32_t tag, lds_u32* flg, const lds_u32* dvc,
+                                                   uint32_t (&idx)[U], bool (&ok)[U]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool live = (nz >> lane) & 1u;
+  const uint32_t r = excl - w0;
+  if (live && excl > w0 && r < kWin * U) flg[r] = tag;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  // Branch-free over the set (the windows' LDS reads can overlap): a window
+  // past T (u > 0 only: next() runs with w0 < T) is located anyway -- its list
+  // index masked into the wave's scratch -- then replaced by window 0.
+  uint32_t f[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) f[u] = flg[u * kWin + lane];  // unconditional: no exec-masked reads
+#pragma unroll
+  for (int u = 0; u < U; u++) f[u] = (f[u] == tag) & (lane != 0u);
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t w = w0 + u * kWin;
+    const uint32_t cw = static_cast<uint32_t>(__builtin_popcountll(uniform64(__ballot(excl <= w) & nz)));
+    const uint64_t b = __ballot(f[u] != 0u);
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
+    const uint32_t d = dvc[(cw + below + f[u] - 1u) & 63u];
+    const uint32_t id = w + lane + d;
+    const uint32_t id0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0));
+    const bool live_w = u == 0 || w < T;  // wave-uniform
+    ok[u] = live_w && w + lane < T;
+    idx[u] = ok[u] ? id : (live_w ? id0 : idx[0]);
+  }
+}
+
 // One wave's walk over a slice's segments in the chunk groups g = g_first,
 // g_first + g_step, ... < g_end (gs <= 64 chunks per group, one per lane: a
 // caller with few chunks per wave shrinks gs so every wave of the workgroup
@@ -579,6 +625,8 @@ struct SegWalk {
   uint32_t g;         // current group (first chunk)
   uint32_t e0;        // next window start in the current group
   lds_u32* scr;       // the wave's kWalkScratch u32 of LDS (DLSM_WALK_LDS)
+  uint32_t tag;       // window sets located so far (seg_locate_set_lds stamps)
+  static constexpr int kFlags = walk_flags<U>();
   uint32_t excl, dv, T;
   uint64_t nz;        // non-empty segments of the current group
   uint32_t nrow;      // prefetched table row pair of group g + g_step (this lane's chunk), packed
@@ -606,7 +654,7 @@ struct SegWalk {
     if (cnt != 0u) {  // compact the non-empty segments' dv (ordered by lane = by excl)
       const uint32_t k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(nz >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(nz), 0u));
-      scr[64 + k] = dv;
+      scr[kFlags + k] = dv;
     }
 #endif
   }
@@ -617,6 +665,13 @@ struct SegWalk {
   __device__ __forceinline__ bool start(uint32_t g_first) {
     g = g_first;
     if (g >= g_end) return false;
+#if DLSM_WALK_LDS
+    if constexpr (kFlags > 64 || (DLSM_WALK_SET && U <= 2)) {
+#pragma unroll
+      for (int u = 0; u < kFlags / 64; u++) scr[u * 64 + (threadIdx.x & 63)] = ~0u;
+      tag = 0;
+    }
+#endif
     const uint32_t row = load_rows(g);
     nrow = load_rows(g + g_step);
     setup(row);
@@ -643,7 +698,10 @@ struct SegWalk {
       }
     }
 #if DLSM_WALK_LDS
-    seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + 64, idx, ok);
+    if constexpr (DLSM_WALK_SET && U <= 2)
+      seg_locate_set_lds<U>(excl, nz, T, e0, tag++, scr, scr + kFlags, idx, ok);
+    else
+      seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + kFlags, idx, ok);
 #else
     seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
 #endif
@@ -1399,6 +1457,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
   const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
+#if DLSM_ABL_NOSTORE
+  uint32_t abl_sink = 0;
+#endif
   walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
       tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch,
       [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
@@ -1446,14 +1507,17 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
         // agree on the count).
 #pragma unroll
         for (int u = 0; u < U; u++)
-#if DLSM_ABL_NOSTORE  // ablation (timing only): almost no answer stores
-          if (ok[u] && ans[u] == 0x12345678u && (hv[u].x & 0xfff) == 0x123u) gmask[idx[u]] = ans[u];
+#if DLSM_ABL_NOSTORE  // ablation (timing only): no answer stores in the walk (folded into one per lane)
+          abl_sink ^= ans[u] + idx[u];
 #elif DLSM_PROBE_UNCOND_STORE
           gmask[idx[u]] = ans[u];
 #else
           if (ok[u]) gmask[idx[u]] = ans[u];
 #endif
       });
+#if DLSM_ABL_NOSTORE
+  if (abl_sink == 0x12345678u) smask[tid] = 1;
+#endif
 }
 
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
