@@ -14,6 +14,8 @@ filter set built once and broadcast to every rank, the ONE 100 M-key lookup
 stream split into N contiguous shards (dlsm_amd/sharding.py).  --scaling weak
 gives every rank its own 16 tables and 100 M lookups instead.
 value = (build keys + probe keys) of the whole job / max-over-ranks wall time.
+A rank whose build batch is under 16 M keys (strong scaling at N >= 2) runs
+its build and probe on two streams (--overlap auto|on|off).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -31,6 +33,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+# A rank's build batch below this many keys leaves the GPU partly idle (its
+# kernels are latency-bound), so the step runs build and probe on two streams:
+# +4 / +9 / +18 % per step at 12.8 / 6.4 / 3.2 M build keys, within +-1 % at
+# the full 25.6 M (profiles/r02_overlap_shares.txt).
+OVERLAP_BELOW = 16_000_000
 
 
 def log(*a):
@@ -76,6 +83,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the all-cores CPU baseline (0 = every host core)")
     ap.add_argument("--cpu-probe-sample", type=int, default=10_000_000)
+    ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
+                    help="run the step's build and probe on two streams (auto: when this rank's build batch "
+                         f"is under {OVERLAP_BELOW // 1_000_000} M keys)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -107,16 +117,21 @@ def main():
     scaling = args.scaling if args.scaling != "auto" else "strong"
 
     N, T, Q, F, bpk = args.keys_per_table, args.tables, args.lookups, args.filters, args.bits_per_key
-    ctx = dlsm_amd.Context(local)
-    ctx.set_path(args.path)
-    if args.probe_round is not None:
-        ctx.set_probe_round(args.probe_round)
-    if args.probe_serial:
-        ctx.set_probe_serial(True)
-    ctx.set_build_groups(args.build_groups)
-    ctx.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
-    stream = torch.cuda.Stream(device=dev)
-    ctx.set_stream(stream)
+
+    def make_ctx():
+        c = dlsm_amd.Context(local)
+        c.set_path(args.path)
+        if args.probe_round is not None:
+            c.set_probe_round(args.probe_round)
+        if args.probe_serial:
+            c.set_probe_serial(True)
+        c.set_build_groups(args.build_groups)
+        c.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
+        st = torch.cuda.Stream(device=dev)
+        c.set_stream(st)
+        return c, st
+
+    ctx, stream = make_ctx()
 
     # ---- inputs, resident in HBM before timing ---------------------------
     t_in = time.time()
@@ -127,33 +142,52 @@ def main():
         f"ready in {time.time() - t_in:.1f}s")
     tables, outs, lens, fs, qk, mask = inp.tables, inp.outs, inp.lens, inp.fs, inp.lookups, inp.mask
 
+    # the build's context and stream: a second pair when the step overlaps
+    # the build with the probe (their buffers are disjoint: the probe reads
+    # the stacked filter set, the build writes the SSTable slots)
+    overlap = bool(tables) and qk.n > 0 and (
+        args.overlap == "on" or (args.overlap == "auto" and len(tables) * N < OVERLAP_BELOW))
+    ctx_b, stream_b = make_ctx() if overlap else (ctx, stream)
+
+    def step():
+        if tables:
+            ctx_b.full_build_dev(tables, outs, lens, bpk)
+        if qk.n:
+            ctx.full_probe_dev(fs, qk, mask)
+
     for _ in range(args.warmup):
-        SH.step(ctx, inp, bpk)
+        step()
     ctx.sync()
+    ctx_b.sync()
 
     # ---- timed region ----------------------------------------------------
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-            torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    evs = [(ev(), ev(), ev(), ev()) for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        evs[i][0].record(stream)
+        evs[i][0].record(stream_b)
         if tables:
-            ctx.full_build_dev(tables, outs, lens, bpk)
-        evs[i][1].record(stream)
+            ctx_b.full_build_dev(tables, outs, lens, bpk)
+        evs[i][1].record(stream_b)
+        evs[i][2].record(stream)
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
-        evs[i][2].record(stream)
+        evs[i][3].record(stream)
+    enqueue_s = time.perf_counter() - t0  # host time to submit the K steps
     stream.synchronize()
+    stream_b.synchronize()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = SH.max_over_ranks(elapsed, dist, dev)
-    build_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in evs]))
-    probe_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs]))
+    build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
 
     # keys of the whole job per step (every rank's share)
     rank_keys = len(tables) * N + qk.n
@@ -197,6 +231,7 @@ def main():
             "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
             "probe_round_keys": args.probe_round, "probe_serial": args.probe_serial,
             "build_groups": args.build_groups,
+            "overlap": overlap,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {
@@ -204,6 +239,7 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
         },
+        "host_enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
                   "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
         "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, qk.n) / probe_ms / 1e3, 1),
@@ -227,9 +263,9 @@ def main():
         # the same build with the job table changing every call (a flush
         # stream hands over new tables each time: the upload is paid)
         result["build"]["rotating_batches_ms"] = round(rotating_build_ms(ctx, stream, tables, outs, lens, bpk), 4)
-        # build and probe of one step on two streams (a flush beside a Get
-        # stream): recorded beside `value`, which stays the sequential step
-        result["overlap"] = overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, local,
+        # the other step shape (two streams if the timed step was sequential):
+        # recorded beside `value`
+        result["overlap_step"] = overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, local,
                                          elapsed / args.steps)
 
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
@@ -413,7 +449,7 @@ def overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, devic
     del ctx2
     nk = len(tables) * tables[0].n + qk.n
     return {"mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 4),
-            "vs_sequential_step": round(seq_step_s / dt, 3),
+            "vs_timed_step": round(seq_step_s / dt, 3),
             "note": "build on a second stream concurrent with the probe; not `value`"}
 
 
