@@ -138,12 +138,18 @@ struct dlsm_ctx {
 
 // A stacked image of the filters of one mask byte that share a line count
 // and probe count (at most 8): filter f answers in bit f % 8 of byte f / 8.
+// A group of 1, 2 or 3-4 filters gets a packed image instead (W = 1, 2 or 4
+// bits per bit position, 64 * W bytes per line: 8 / 4 / 2 times the lines per
+// LDS slice), so a large single filter -- the biggest file of a level -- still
+// fits the sliced path, and small groups walk fewer, longer bucket runs.
 struct ProbeGroup {
-  uint64_t* stacked = nullptr;  // L*64 u64 words
+  uint64_t* stacked = nullptr;  // L * 8 * 2^lgw u64 words
   uint32_t L = 0, magic = 0;
   int k = 0;
   int mask_byte = 0;
   bool first_of_byte = false;  // writes its mask byte; later groups of the byte OR into it
+  int lgw = 3;                  // log2 bits per bit position of the image (3: stacked bytes)
+  uint32_t slotmap = 0;         // packed images: member m answers in bit (slotmap >> 4m) & 7
 };
 
 struct dlsm_filterset {
@@ -1031,6 +1037,10 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
             done[q - 8 * b] = true;
             m.push_back(q);
           }
+        const int nm = static_cast<int>(m.size());
+        g.lgw = nm == 1 ? 0 : nm == 2 ? 1 : nm <= 4 ? 2 : 3;
+        if (const char* e = getenv("DLSM_PROBE_PACKED"); e && atoi(e) == 0) g.lgw = 3;  // A/B knob
+        for (int j = 0; j < nm && g.lgw < 3; j++) g.slotmap |= static_cast<uint32_t>(m[j] % 8) << (4 * j);
         fs->groups.push_back(g);
         members.push_back(m);
       }
@@ -1045,9 +1055,12 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
     if (e == hipSuccess)
       e = hipMemcpyAsync(fs->d_slots, slots.data(), sizeof(FilterDev) * slots.size(), hipMemcpyHostToDevice, s);
     for (size_t g = 0; g < G && e == hipSuccess; g++) {
-      const uint64_t bytes = static_cast<uint64_t>(fs->groups[g].L) * 512u;
-      e = hipMalloc(reinterpret_cast<void**>(&fs->groups[g].stacked), bytes);
-      if (e == hipSuccess) e = launch_stack_filters(fs->d_slots + 8 * g, fs->groups[g].L, fs->groups[g].stacked, s);
+      ProbeGroup& grp = fs->groups[g];
+      const uint64_t bytes = static_cast<uint64_t>(grp.L) * (64u << grp.lgw);
+      e = hipMalloc(reinterpret_cast<void**>(&grp.stacked), bytes);
+      if (e == hipSuccess)
+        e = grp.lgw == 3 ? launch_stack_filters(fs->d_slots + 8 * g, grp.L, grp.stacked, s)
+                         : launch_pack_filters(fs->d_slots + 8 * g, grp.slotmap, grp.lgw, grp.L, grp.stacked, s);
       fs->stacked_bytes += bytes;
     }
   }
@@ -1081,10 +1094,17 @@ int dlsm_filterset_size(const dlsm_filterset* fs, int* n_filters, uint64_t* devi
 
 namespace {
 
-// Slices of 2^lgR stacked lines for a group of line count L (a table with
-// more than kMaxSlices slices of 64 KiB moves to 128 KiB slices, one
-// workgroup per CU); 0 when the group cannot be sliced.
-uint32_t group_slices(const dlsm_ctx* ctx, uint32_t L, int* lgR) {
+// Slices of 2^lgR image lines for a group of line count L (a byte-wide
+// stacked table with more than kMaxSlices slices of 64 KiB moves to 128 KiB
+// slices, one workgroup per CU; packed images always use 128 KiB slices of
+// 2^(11 - lgw) lines); 0 when the group cannot be sliced.
+uint32_t group_slices(const dlsm_ctx* ctx, const ProbeGroup& g, int* lgR) {
+  const uint32_t L = g.L;
+  if (g.lgw < 3) {
+    *lgR = 11 - g.lgw;
+    const uint32_t S = ceil_div_u32(L, 1u << *lgR);
+    return S >= 1 && S <= kMaxSlices ? S : 0;
+  }
   *lgR = ctx->probe_lgr;
   uint32_t S = ceil_div_u32(L, 1u << *lgR);
   if (S > kMaxSlices && *lgR < 8) {
@@ -1131,7 +1151,7 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   uint32_t Smax = 0;
   for (const auto& g : fs->groups) {
     int lg;
-    Smax = std::max(Smax, group_slices(ctx, g.L, &lg));
+    Smax = std::max(Smax, group_slices(ctx, g, &lg));
   }
   const uint64_t rstride = static_cast<uint64_t>(nC) * probe_region(static_cast<uint32_t>(C));
   DLSM_CHECK(ctx->entries.ensure(rstride));
@@ -1141,7 +1161,7 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   for (size_t gi = 0; gi < fs->groups.size(); gi++) {
     const ProbeGroup& g = fs->groups[gi];
     int lgR;
-    const uint32_t S = group_slices(ctx, g.L, &lgR);
+    const uint32_t S = group_slices(ctx, g, &lgR);
     if (S == 0 || ctx->path == 1) {
       DLSM_TRY(launch_probe_direct_group(fs->d_slots + 8 * gi, hk, mask_dev, mb, g.mask_byte,
                                          g.first_of_byte, s));
@@ -1149,8 +1169,8 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
     }
     DLSM_TRY(launch_probe_partition(hk, g.L, g.magic, lgR, S, ctx->entries.p, ctx->pos.p, ctx->tab.p,
                                     KM_HASH, lgC, s));
-    DLSM_TRY(launch_probe_slices(g.stacked, g.L, g.magic, g.k, lgR, S, nC, ctx->entries.p, ctx->tab.p,
-                                 ctx->smask.p, slice_parts(S, nC, lgR), lgC, s));
+    DLSM_TRY(launch_probe_slices(g.stacked, g.L, g.magic, g.k, lgR, g.lgw, g.slotmap, S, nC, ctx->entries.p,
+                                 ctx->tab.p, ctx->smask.p, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute_group(n, ctx->pos.p, ctx->smask.p, mask_dev, mb, g.mask_byte,
                                           g.first_of_byte, lgC, s));
   }
@@ -1177,7 +1197,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   bool all_sliceable = !fs->groups.empty();
   for (const auto& grp : fs->groups) {
     int lg;
-    all_sliceable = all_sliceable && group_slices(ctx, grp.L, &lg) != 0;
+    all_sliceable = all_sliceable && group_slices(ctx, grp, &lg) != 0;
   }
   if (ctx->path == 2 && !(all_sliceable && fits)) return DLSM_E_ARG;
   if (fs->groups.empty() || ctx->path == 1 || !fits) {
@@ -1190,7 +1210,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   // hashed inside the partition pass.
   const ProbeGroup& grp = fs->groups[0];
   int lgR;
-  const uint32_t S = group_slices(ctx, grp.L, &lgR);
+  const uint32_t S = group_slices(ctx, grp, &lgR);
   // Rounds of probe_round keys, pipelined: round r's partition (helper
   // stream) overlaps round r-1's slice + unpermute (context stream), or
   // serial (DLSM_OPT_PROBE_ROUND_SERIAL).  A round's intermediates (4 B hash +
@@ -1230,8 +1250,8 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
     DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, lgR, S, ent, pos, tab, mode, lgC, ps));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
-    DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, S, nC, ent, tab, sm,
-                                 slice_parts(S, nC, lgR), lgC, s));
+    DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, grp.lgw, grp.slotmap, S, nC, ent,
+                                 tab, sm, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }

@@ -134,6 +134,12 @@ hipError_t launch_probe_direct_group(const FilterDev* slots, KeyDesc hashes, uin
 // filter whose answer goes to bit b of the answer byte, or has data == nullptr
 // (bit b stays 0).
 hipError_t launch_stack_filters(const FilterDev* slots, uint32_t L, uint64_t* stacked, hipStream_t s);
+// Packed image of a group of at most 2^lgw (< 8) filters of one line count:
+// each line holds 512 fields of W = 2^lgw bits (64 * W bytes), field bit m =
+// the line's bit of member m, whose slot is (slotmap >> 4m) & 7 (members past
+// the group's size, or with data == nullptr, read as 0).
+hipError_t launch_pack_filters(const FilterDev* slots, uint32_t slotmap, int lgw, uint32_t L,
+                               uint64_t* packed, hipStream_t s);
 // BloomHash of every key (u32 per key, coalesced): the grouped probe hashes
 // each lookup once and partitions the hashes once per filter group.
 hipError_t launch_probe_hash(KeyDesc keys, uint32_t* hashes, int mode, hipStream_t s);
@@ -143,12 +149,15 @@ hipError_t launch_probe_hash(KeyDesc keys, uint32_t* hashes, int mode, hipStream
 hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                         uint8_t* mask, int stride, int byte, bool first, int lgC,
                                         hipStream_t s);
-// lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice (7, 8).
+// lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice
+// (7, 8 for byte-wide stacked images; 11 - lgw for packed ones, lgw < 3).
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                   uint16_t* tab, int mode, int lgC, hipStream_t s);
+// lgw 3: byte-wide stacked image (launch_stack_filters); lgw 0..2: packed
+// image (launch_pack_filters) whose member m answers in bit (slotmap >> 4m) & 7.
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
-                               int lgR, uint32_t n_slices, uint32_t n_chunks,
+                               int lgR, int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
                                int parts, int lgC, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,

@@ -1227,10 +1227,18 @@ __global__ __launch_bounds__(kBlock) void stack_filters_kernel(const FilterDev* 
 // positions are (e + q * (e >> 17)) & 511, exactly those of h.
 // Bit 31 is never read either: valid entries clear it, and the bucket
 // padding is kProbePadEntry (bit 31 set; its answer byte is never read).
+// Packed images (fewer than 5 filters per group, 512 / 1,024 / 2,048 lines
+// per slice) need offsets up to 2^11: the high 3 bits go to [26, 29), which
+// a probe never reads either (only delta mod 512 matters).
 constexpr uint32_t kEntryLineMask = 0xffu << 9;
+constexpr uint32_t kEntryLineHiMask = 7u << 26;
 constexpr uint32_t kProbePadEntry = 0x80000000u;
 __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
-  return (h & ~(kEntryLineMask | kProbePadEntry)) | (line_off << 9);
+  return (h & ~(kEntryLineMask | kEntryLineHiMask | kProbePadEntry)) | ((line_off & 0xffu) << 9) |
+         ((line_off >> 8) << 26);
+}
+__device__ __forceinline__ uint32_t probe_entry_off(uint32_t e) {
+  return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
 }
 
 // Phase timestamps of the persistent probe partition (diagnostic builds only,
@@ -1410,21 +1418,45 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   }
 }
 
+// One probe of a packed image (LGW < 3): the W-bit field of position p in
+// the line at LDS byte `base`, shifted down to bit 0 (higher bits are the
+// next fields: the caller masks after the AND of the k probes).
+template <int LGW>
+__device__ __forceinline__ uint32_t packed_probe(const uint8_t* sl, uint32_t base, uint32_t x) {
+  const uint32_t p = x & 511u;
+  return static_cast<uint32_t>(sl[base + (p >> (3 - LGW))]) >> ((p << LGW) & 7u);
+}
+// The group's answer byte from a packed image's W-bit field: member m's bit
+// goes to its slot bit (slotmap >> 4m) & 7.
+template <int LGW>
+__device__ __forceinline__ uint32_t packed_answer(uint32_t acc, uint32_t slotmap) {
+  uint32_t a = 0;
+#pragma unroll
+  for (int m = 0; m < (1 << LGW); m++) a |= ((acc >> m) & 1u) << ((slotmap >> (4 * m)) & 7u);
+  return a;
+}
+
 // Pass 2: one NT-thread workgroup per (slice of 2^LGR stacked lines, part of
-// the chunks of C keys); the slice (R x 512 B: 64 or 128 KiB) sits in LDS, waves walk the slice's
-// segments of 64 chunks at a time, 6 windows of 63 hashes in flight per wave.
-// smask gets each key's F-bit answer at the key's bucketed position.
-template <int LGR, int K, int NT, int C>
+// the chunks of C keys); the slice (R lines x 64 * 2^LGW B: 64 or 128 KiB)
+// sits in LDS, waves walk the slice's segments of 64 chunks at a time.
+// smask gets each key's answer byte at the key's bucketed position.
+// LGW 3: byte-wide stacked image (up to 8 filters, one byte per bit position);
+// LGW 0..2: packed image of a group of 1, 2 or 3-4 filters (a W-bit field per
+// bit position: 8 / 4 / 2 times the lines per slice), whose member m answers
+// in bit (slotmap >> 4m) & 7.
+template <int LGR, int LGW, int K, int NT, int C>
 __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
-    const uint8_t* __restrict__ stacked, uint32_t L, uint32_t magic, int k, uint32_t S,
+    const uint8_t* __restrict__ stacked, uint32_t L, uint32_t slotmap, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
   constexpr uint32_t R = 1u << LGR;
+  constexpr uint32_t LB = 64u << LGW;  // bytes per line of the image
+  static_assert(LGW == 3 || LGR + LGW == 11, "packed images use 128 KiB slices");
   // window units in flight per wave: one 128 KiB slice per CU (LGR 8) leaves
   // 4 waves per SIMD, so each carries two windows (measured best per shape)
-  constexpr int U = LGR >= 8 ? kProbeWalkU8 : kProbeWalkU;
+  constexpr int U = LGR + LGW >= 11 ? kProbeWalkU8 : kProbeWalkU;
   constexpr int NW = NT / 64;
-  __shared__ __attribute__((aligned(16))) uint8_t sl[R * 512];
+  __shared__ __attribute__((aligned(16))) uint8_t sl[R * LB];
   __shared__ uint32_t walk_scr[NW * kWalkScratch];
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
@@ -1438,10 +1470,10 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     // Loads AND stores are clamped (lanes past the slice rewrite its last
     // unit with the same bytes): a store under a branch let the compiler sink
     // each load into its branch, one HBM round trip per load.
-    constexpr int V = R * 32 / NT;
-    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * 512u);
+    constexpr int V = R * (LB / 16) / NT;
+    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * LB);
     uint4* dst = reinterpret_cast<uint4*>(sl);
-    const uint32_t nw = nl * 32u;
+    const uint32_t nw = nl * (LB / 16);
     uint4 t[V];
 #pragma unroll
     for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
@@ -1472,8 +1504,26 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
 #pragma unroll
           for (int j = 0; j < 4; j++) {
             uint32_t x = e4[j];
-            const uint32_t base = x & ((R - 1u) << 9);  // line offset * 512 stacked bytes (probe_entry)
             const uint32_t delta = x >> 17;            // low 9 bits of rotr(h, 17)
+            if constexpr (LGW < 3) {
+              const uint32_t base = probe_entry_off(x) * LB;
+              uint32_t acc = ~0u;
+              if constexpr (K > 0) {
+#pragma unroll
+                for (int q = 0; q < K; q++) {
+                  acc &= packed_probe<LGW>(sl, base, x);
+                  x += delta;
+                }
+              } else {
+                for (int q = 0; q < k; q++) {
+                  acc &= packed_probe<LGW>(sl, base, x);
+                  x += delta;
+                }
+              }
+              a |= packed_answer<LGW>(acc, slotmap) << (8 * j);
+              continue;
+            }
+            const uint32_t base = x & ((R - 1u) << 9);  // line offset * 512 stacked bytes (probe_entry)
             uint32_t acc = 0xffu;
             if constexpr (K > 0) {
 #pragma unroll
@@ -1837,6 +1887,43 @@ hipError_t launch_stack_filters(const FilterDev* slots, uint32_t L, uint64_t* st
   return hipGetLastError();
 }
 
+// Packed image of 1, 2 or up to 4 filters (W = 2^lgw bits per bit position):
+// bit m of field p of line l = bit p of line l of member m (the filter's own
+// layout: byte p >> 3, bit p & 7, util/bloom_impl.h:427-443).  W = 1 is the
+// filter's bytes unchanged.  One u64 word (64 / W positions) per thread; the
+// image is built once per filter set.
+__global__ __launch_bounds__(kBlock) void pack_filters_kernel(const FilterDev* __restrict__ slots,
+                                                              uint32_t slotmap, int lgw, uint64_t words,
+                                                              uint64_t* __restrict__ packed) {
+  const int W = 1 << lgw;
+  const uint8_t* src[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int m = 0; m < W; m++) src[m] = slots[(slotmap >> (4 * m)) & 7u].data;
+  const uint64_t per_line = 8u << lgw;  // u64 words per line (64 * W bytes)
+  for (uint64_t w = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; w < words;
+       w += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    const uint64_t line = w / per_line;
+    const uint32_t p0 = static_cast<uint32_t>(w % per_line) * (64u >> lgw);  // first position of the word
+    uint64_t x = 0;
+    for (int m = 0; m < W; m++) {
+      if (!src[m]) continue;
+      const uint8_t* ln = src[m] + line * 64u;
+      for (uint32_t i = 0; i < (64u >> lgw); i++) {
+        const uint32_t pp = p0 + i;
+        x |= static_cast<uint64_t>((ln[pp >> 3] >> (pp & 7u)) & 1u) << ((i << lgw) + m);
+      }
+    }
+    packed[w] = x;
+  }
+}
+
+hipError_t launch_pack_filters(const FilterDev* slots, uint32_t slotmap, int lgw, uint32_t L,
+                               uint64_t* packed, hipStream_t s) {
+  if (lgw < 0 || lgw > 2) return hipErrorInvalidValue;
+  const uint64_t words = static_cast<uint64_t>(L) * (8u << lgw);
+  pack_filters_kernel<<<grid_for(words), kBlock, 0, s>>>(slots, slotmap, lgw, words, packed);
+  return hipGetLastError();
+}
+
 // Hash pass of the grouped probe: one 512-thread workgroup per 4,096 keys,
 // the key tiles staged through LDS like the partition's (K20 / K28), the
 // hashes stored coalesced.
@@ -1948,37 +2035,41 @@ hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int 
   }
 }
 
-template <int LGR, int C>
-static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
+template <int LGR, int LGW, int C>
+static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t slotmap, int k,
                                   uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
                                   const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stacked);
   constexpr int NT = DLSM_PROBE_NT;
   if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
-    probe_slice_kernel<LGR, 6, NT, C><<<n_slices * parts, NT, 0, s>>>(
-        st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
+    probe_slice_kernel<LGR, LGW, 6, NT, C><<<n_slices * parts, NT, 0, s>>>(
+        st, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
   else
-    probe_slice_kernel<LGR, 0, NT, C><<<n_slices * parts, NT, 0, s>>>(
-        st, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts);
+    probe_slice_kernel<LGR, LGW, 0, NT, C><<<n_slices * parts, NT, 0, s>>>(
+        st, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
 
-hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR,
-                               uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
-                               const uint16_t* tab, uint8_t* smask, int parts, int lgC,
-                               hipStream_t s) {
+hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR, int lgw,
+                               uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
+                               const uint32_t* entries, const uint16_t* tab, uint8_t* smask, int parts,
+                               int lgC, hipStream_t s) {
+  (void)magic;  // the partition already reduced every hash to its slice and line
   if (n_chunks == 0) return hipSuccess;
-#define DLSM_SLICES(LG, CC) \
-  return probe_slices_as<LG, CC>(stacked, L, magic, k, n_slices, n_chunks, entries, tab, smask, parts, s)
-  if (lgR == 7) {
-    if (lgC == 12) DLSM_SLICES(7, 4096);
-    if (lgC == 13) DLSM_SLICES(7, 8192);
-    if (lgC == 14) DLSM_SLICES(7, 16384);
-  } else if (lgR == 8) {
-    if (lgC == 12) DLSM_SLICES(8, 4096);
-    if (lgC == 13) DLSM_SLICES(8, 8192);
-    if (lgC == 14) DLSM_SLICES(8, 16384);
-  }
+#define DLSM_SLICES(LG, LW, CC) \
+  return probe_slices_as<LG, LW, CC>(stacked, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts, s)
+#define DLSM_SLICES_C(LG, LW)                  \
+  do {                                         \
+    if (lgC == 12) DLSM_SLICES(LG, LW, 4096);  \
+    if (lgC == 13) DLSM_SLICES(LG, LW, 8192);  \
+    if (lgC == 14) DLSM_SLICES(LG, LW, 16384); \
+  } while (0)
+  if (lgw == 3 && lgR == 7) DLSM_SLICES_C(7, 3);
+  if (lgw == 3 && lgR == 8) DLSM_SLICES_C(8, 3);
+  if (lgw == 2 && lgR == 9) DLSM_SLICES_C(9, 2);
+  if (lgw == 1 && lgR == 10) DLSM_SLICES_C(10, 1);
+  if (lgw == 0 && lgR == 11) DLSM_SLICES_C(11, 0);
+#undef DLSM_SLICES_C
 #undef DLSM_SLICES
   return hipErrorInvalidValue;
 }
