@@ -86,6 +86,9 @@ def main():
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
                     help="run the step's build and probe on two streams (auto: when this rank's build batch "
                          f"is under {OVERLAP_BELOW // 1_000_000} M keys)")
+    ap.add_argument("--cosched", type=int, default=0,
+                    help="co-schedule build and probe on CU-masked streams: the build's slice pass on this "
+                         "many CUs per XCD (1..4), every partition pass on the other CUs (0 = off)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -147,7 +150,25 @@ def main():
     # the stacked filter set, the build writes the SSTable slots)
     overlap = bool(tables) and qk.n > 0 and (
         args.overlap == "on" or (args.overlap == "auto" and len(tables) * N < OVERLAP_BELOW))
-    ctx_b, stream_b = make_ctx() if overlap else (ctx, stream)
+    cosched = args.cosched if (tables and qk.n > 0) else 0
+    part_stream = None
+    if cosched:
+        # the build's LDS-bound slice pass on a few CUs of every XCD (its own
+        # context and stream), every HBM-bound partition pass -- build and
+        # probe -- on the other CUs, the probe's slice / unpermute on all
+        overlap = True
+        n_cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        small = dlsm_amd.cu_subset(cosched, n_cus)
+        big = sorted(set(range(n_cus)) - set(small))
+        ctx_b = dlsm_amd.Context(local)
+        ctx_b.set_path(args.path)
+        stream_b = dlsm_amd.cu_mask_stream(local, small, n_cus)
+        part_stream = dlsm_amd.cu_mask_stream(local, big, n_cus)
+        ctx_b.set_stream(stream_b)
+        for c in (ctx, ctx_b):
+            c.set_partition_stream(part_stream, len(big))
+    else:
+        ctx_b, stream_b = make_ctx() if overlap else (ctx, stream)
 
     def step():
         if tables:
@@ -178,14 +199,32 @@ def main():
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
         evs[i][3].record(stream)
+        if cosched:
+            # the next build partition starts behind this probe's slice /
+            # unpermute passes (co-running with them slows both)
+            stream_b.wait_event(evs[i][3])
     enqueue_s = time.perf_counter() - t0  # host time to submit the K steps
     stream.synchronize()
     stream_b.synchronize()
+    if part_stream is not None:
+        part_stream.synchronize()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = SH.max_over_ranks(elapsed, dist, dev)
+    if cosched:
+        # co-scheduled passes overlap, so the per-pass times (roofline) come
+        # from the same K steps run one pass after another on one stream
+        ctx.set_partition_stream(None)
+        for i in range(args.steps):
+            evs[i][0].record(stream)
+            ctx.full_build_dev(tables, outs, lens, bpk)
+            evs[i][1].record(stream)
+            evs[i][2].record(stream)
+            ctx.full_probe_dev(fs, qk, mask)
+            evs[i][3].record(stream)
+        stream.synchronize()
     build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
 
@@ -232,6 +271,7 @@ def main():
             "probe_round_keys": args.probe_round, "probe_serial": args.probe_serial,
             "build_groups": args.build_groups,
             "overlap": overlap,
+            "cosched_build_slice_cus_per_xcd": cosched,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {

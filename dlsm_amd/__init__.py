@@ -96,6 +96,29 @@ def _ptr(x) -> Optional[int]:
     return int(x.data_ptr())
 
 
+def cu_subset(per_xcd: int, n_cus: int = 256, n_xcds: int = 8) -> list:
+    """per_xcd compute units on each XCD under both CU-mask numberings a
+    multi-XCD part may use (bit i on XCD i // (n_cus / n_xcds), or on XCD
+    i % n_xcds): i = (n_cus / n_xcds) x + n_xcds j + x, j < per_xcd <= 4."""
+    per = n_cus // n_xcds
+    if not 1 <= per_xcd <= per // n_xcds:
+        raise ValueError(f"per_xcd must be in [1, {per // n_xcds}]")
+    return sorted(per * x + n_xcds * j + x for x in range(n_xcds) for j in range(per_xcd))
+
+
+def cu_mask_stream(device: int, cus, n_cus: int = 256):
+    """A torch ExternalStream over a new hipStream_t restricted to the CUs in
+    `cus` (dlsm_stream_create_cu_mask).  The stream lives as long as the process."""
+    import torch
+
+    words = (C.c_uint32 * ((n_cus + 31) // 32))()
+    for i in cus:
+        words[i // 32] |= 1 << (i % 32)
+    raw = C.c_void_p()
+    check(lib().dlsm_stream_create_cu_mask(device, words, len(words), C.byref(raw)), "cu_mask_stream")
+    return torch.cuda.ExternalStream(raw.value, device=torch.device("cuda", device))
+
+
 @dataclass
 class Keys:
     """A packed key set: ``data`` (uint8) + ``offsets`` (uint64[n+1]) or fixed ``key_len``.
@@ -271,6 +294,12 @@ class Context:
         """Run on a torch.cuda.Stream (or its raw handle); None = own stream."""
         raw = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
         check(lib().dlsm_ctx_set_stream(self.h, raw), "set_stream")
+
+    def set_partition_stream(self, stream=None, cus: int = 0):
+        """Partition passes on `stream` (a CU-masked stream: cu_mask_stream),
+        slice / unpermute passes on the context stream; None = one stream."""
+        raw = None if stream is None else (stream if isinstance(stream, int) else stream.cuda_stream)
+        check(lib().dlsm_ctx_set_partition_stream(self.h, raw, cus if raw else 0), "set_partition_stream")
 
     @property
     def stream_handle(self) -> int:

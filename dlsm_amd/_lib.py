@@ -67,6 +67,9 @@ SIGNATURES = [
     ("dlsm_ctx_set_stream", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_stream", _VP, [_VP]),
     ("dlsm_ctx_sync", C.c_int, [_VP]),
+    ("dlsm_ctx_set_partition_stream", C.c_int, [_VP, _VP, C.c_uint32]),
+    ("dlsm_stream_create_cu_mask", C.c_int, [C.c_int, C.POINTER(C.c_uint32), C.c_uint32, C.POINTER(_VP)]),
+    ("dlsm_stream_destroy", C.c_int, [_VP]),
     ("dlsm_ctx_reserve", C.c_int, [_VP, C.c_uint64, C.c_uint32]),
     ("dlsm_ctx_stats", C.c_int, [_VP, _U64P, _U64P]),
     ("dlsm_ctx_set_path", C.c_int, [_VP, C.c_int]),

@@ -90,6 +90,12 @@ struct dlsm_ctx {
   hipEvent_t ev_fork = nullptr;           // context stream -> helper
   hipEvent_t ev_part[kStageEvents] = {};  // partition of buffer / group b done (helper)
   hipEvent_t ev_free[kStageEvents] = {};  // buffer b consumed (context stream)
+  // dlsm_ctx_set_partition_stream: the partition passes run on pstream
+  // (typically restricted to a CU subset), the rest on the context stream
+  hipStream_t pstream = nullptr;
+  uint32_t pcus = 0;                      // CUs the persistent partition grid is sized for (0: all)
+  hipEvent_t ev_pfork = nullptr;          // context stream -> pstream
+  hipEvent_t ev_pdone = nullptr;          // partition done (pstream -> context stream)
   int path = 0;
   int build_groups = 1;     // job groups of a build (1 = one partition + one slice launch)
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
@@ -253,6 +259,21 @@ int fork_aux(dlsm_ctx* ctx) {
 }
 
 // `to` waits for everything queued on `from` so far.
+// dlsm_ctx_set_partition_stream: the partition stream starts behind
+// everything queued on the context stream (the call's inputs, and the
+// previous call's consumers of the workspace it overwrites) ...
+int fork_part(dlsm_ctx* ctx) {
+  DLSM_TRY(hipEventRecord(ctx->ev_pfork, ctx->stream));
+  DLSM_TRY(hipStreamWaitEvent(ctx->pstream, ctx->ev_pfork, 0));
+  return DLSM_OK;
+}
+// ... and the context stream's next pass starts behind the partition.
+int join_part(dlsm_ctx* ctx) {
+  DLSM_TRY(hipEventRecord(ctx->ev_pdone, ctx->pstream));
+  DLSM_TRY(hipStreamWaitEvent(ctx->stream, ctx->ev_pdone, 0));
+  return DLSM_OK;
+}
+
 int hand_over(hipStream_t from, hipStream_t to, hipEvent_t ev) {
   DLSM_TRY(hipEventRecord(ev, from));
   DLSM_TRY(hipStreamWaitEvent(to, ev, 0));
@@ -355,6 +376,8 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_pdone, hipEventDisableTiming);
   for (int b = 0; b < kStageEvents && e == hipSuccess; b++) {
     e = hipEventCreateWithFlags(&ctx->ev_part[b], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_free[b], hipEventDisableTiming);
@@ -377,6 +400,7 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   DeviceGuard g(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->aux) (void)hipStreamSynchronize(ctx->aux);
+  if (ctx->pstream) (void)hipStreamSynchronize(ctx->pstream);
   ctx->entries.release();
   ctx->tab.release();
   ctx->jobs.release();
@@ -400,6 +424,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->crc_cap.release();
   ctx->crc_val.release();
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_pfork) (void)hipEventDestroy(ctx->ev_pfork);
+  if (ctx->ev_pdone) (void)hipEventDestroy(ctx->ev_pdone);
   for (int b = 0; b < kStageEvents; b++) {
     if (ctx->ev_part[b]) (void)hipEventDestroy(ctx->ev_part[b]);
     if (ctx->ev_free[b]) (void)hipEventDestroy(ctx->ev_free[b]);
@@ -418,6 +444,31 @@ int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* s) {
 }
 
 void* dlsm_ctx_stream(dlsm_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+int dlsm_ctx_set_partition_stream(dlsm_ctx* ctx, void* s, uint32_t cus) {
+  if (!ctx) return DLSM_E_ARG;
+  ctx->pstream = static_cast<hipStream_t>(s);
+  ctx->pcus = s ? cus : 0u;
+  return DLSM_OK;
+}
+
+int dlsm_stream_create_cu_mask(int device, const uint32_t* mask, uint32_t words, void** out) {
+  if (!out || !mask || words == 0) return DLSM_E_ARG;
+  *out = nullptr;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) return DLSM_E_DEVICE;
+  DeviceGuard g(device);
+  hipStream_t st = nullptr;
+  DLSM_TRY(hipExtStreamCreateWithCUMask(&st, words * 32u, mask));
+  *out = st;
+  return DLSM_OK;
+}
+
+int dlsm_stream_destroy(void* s) {
+  if (!s) return DLSM_E_ARG;
+  DLSM_TRY(hipStreamDestroy(static_cast<hipStream_t>(s)));
+  return DLSM_OK;
+}
 
 int dlsm_ctx_sync(dlsm_ctx* ctx) {
   if (!ctx) return DLSM_E_ARG;
@@ -655,13 +706,19 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     const int ng = static_cast<int>(cut.size()) - 1;
     auto chunk_at = [&](int j) { return j < n_jobs ? starts[j] : chunk; };
     auto slice_at = [&](int j) { return j < n_jobs ? starts[n_jobs + j] : slice; };
-    if (exact) DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, s));
+    // partition stream (dlsm_ctx_set_partition_stream, one job group): the
+    // count and partition passes there, the slices on the context stream
+    const bool split = ctx->pstream && ng == 1;
+    hipStream_t ps = split ? ctx->pstream : s;
+    if (split) DLSM_CHECK(fork_part(ctx));
+    if (exact) DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, ps));
     if (ng > 1) DLSM_CHECK(fork_aux(ctx));
     for (int g = 0; g < ng; g++) {
       const uint32_t c0 = chunk_at(cut[g]), s0 = slice_at(cut[g]);
       DLSM_TRY(launch_full_partition(ctx->jobs.p, chunk0s, n_jobs, c0, chunk_at(cut[g + 1]) - c0,
                                      ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, mode, exact,
-                                     ng > 1 ? ctx->aux : s));
+                                     ng > 1 ? ctx->aux : ps));
+      if (split) DLSM_CHECK(join_part(ctx));
       if (ng > 1) DLSM_CHECK(hand_over(ctx->aux, s, ctx->ev_part[g % kStageEvents]));
       DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, s0, slice_at(cut[g + 1]) - s0,
                                   ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, s));
@@ -1233,7 +1290,11 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   DLSM_CHECK(ctx->smask.ensure(rstride * nbuf));
   DLSM_CHECK(ctx->tab.ensure(tstride * nbuf));
   if (pipe) DLSM_CHECK(fork_aux(ctx));
-  hipStream_t ps = pipe ? ctx->aux : s;
+  // dlsm_ctx_set_partition_stream (one round): the partition there, the
+  // slice + unpermute passes on the context stream
+  const bool split = ctx->pstream && n_rounds == 1;
+  if (split) DLSM_CHECK(fork_part(ctx));
+  hipStream_t ps = pipe ? ctx->aux : (split ? ctx->pstream : s);
   for (uint64_t r = 0; r < n_rounds; r++) {
     const uint64_t r0 = r * round;
     const uint64_t nr = std::min(round, n - r0);
@@ -1248,8 +1309,10 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     if (kd.offsets) kr.offsets = kd.offsets + r0;
     else kr.bytes = kd.bytes + r0 * kd.key_len;
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
-    DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, lgR, S, ent, pos, tab, mode, lgC, ps));
+    DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, lgR, S, ent, pos, tab, mode, lgC, ps,
+                                    split ? ctx->pcus : 0u));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
+    if (split) DLSM_CHECK(join_part(ctx));
     DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, grp.lgw, grp.slotmap, S, nC, ent,
                                  tab, sm, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));

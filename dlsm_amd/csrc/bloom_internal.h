@@ -153,7 +153,8 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
 // (7, 8 for byte-wide stacked images; 11 - lgw for packed ones, lgw < 3).
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint16_t* tab, int mode, int lgC, hipStream_t s);
+                                  uint16_t* tab, int mode, int lgC, hipStream_t s,
+                                  uint32_t cus = 0);  // CUs the persistent grid is sized for (0: the device's)
 // lgw 3: byte-wide stacked image (launch_stack_filters); lgw 0..2: packed
 // image (launch_pack_filters) whose member m answers in bit (slotmap >> 4m) & 7.
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,

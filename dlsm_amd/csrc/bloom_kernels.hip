@@ -962,7 +962,16 @@ __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint
 // ---------------------------------------------------------------------------
 constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
 // probe slices: 64 KiB LDS per workgroup, 512 or 1024 threads (launch_probe_slices)
-constexpr int kWalkU = 8;               // hashes in flight per lane (build segment walk)
+#ifndef DLSM_BUILD_WALKU
+#define DLSM_BUILD_WALKU 8
+#endif
+#ifndef DLSM_BUILD_DEPTH
+#define DLSM_BUILD_DEPTH 1  // window sets of entry loads in flight per wave (build walk)
+#endif
+#ifndef DLSM_BUILD_GS
+#define DLSM_BUILD_GS 0     // chunks per wave group for jobs of >= 256 chunks (0: 64)
+#endif
+constexpr int kWalkU = DLSM_BUILD_WALKU;  // hashes in flight per lane (build segment walk)
 #ifndef DLSM_PROBE_U
 #define DLSM_PROBE_U 1
 #endif
@@ -1020,11 +1029,13 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       // chunks per wave group: every wave gets a share of a small job's chunks
       // (a job of >= 256 chunks keeps whole 64-chunk groups: measured 2 %
       // faster at 391 chunks than 8 groups of 49, gpurun_out v19b)
-      const uint32_t gs = nC >= 256u ? 64u : max(1u, (nC + NW - 1) / NW);
+      const uint32_t gs = nC >= 256u ? (DLSM_BUILD_GS ? min(64u, max(1u, (nC + NW - 1) / NW))
+                                                        : 64u)
+                                     : max(1u, (nC + NW - 1) / NW);
 #if DLSM_BUILD_UNITS
       // 16-byte units of 4 entries per lane per load (padding entries skipped)
       constexpr int U4 = kWalkU / 4;
-      walk_segments<U4, kBuildRegion / 4, uint4>(
+      walk_segments<U4, kBuildRegion / 4, uint4, DLSM_BUILD_DEPTH>(
           tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs, walk_scr + wv * kWalkScratch,
           [&](const uint4 (&hv)[U4], const uint32_t (&)[U4], const bool (&ok)[U4], uint32_t) {
             if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
@@ -1984,7 +1995,7 @@ static uint32_t device_cus() {
 template <int C, int NT, int H = 1>
 static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                      uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                     uint16_t* tab, int mode, hipStream_t s) {
+                                     uint16_t* tab, int mode, hipStream_t s, uint32_t cus) {
   const uint32_t nC = static_cast<uint32_t>((keys.n + C - 1) / C);
   if (nC == 0) return hipSuccess;
   // persistent: a few resident workgroups per CU loop over the chunks
@@ -1993,7 +2004,7 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
     const char* e = getenv("DLSM_PART_GRID_PER_CU");
     return e ? static_cast<uint32_t>(atoi(e)) : 2u;
   }();
-  const uint32_t g = per_cu ? std::min(nC, per_cu * device_cus()) : nC;
+  const uint32_t g = per_cu ? std::min(nC, per_cu * (cus ? cus : device_cus())) : nC;
   // $DLSM_PROBE_PLAIN_STORES=1: plain (Infinity-Cache-allocating) intermediate
   // stores, for round-sized batches (A/B knob; K20 keys only)
   static const bool plain = [] {
@@ -2020,17 +2031,17 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
 
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint16_t* tab, int mode, int lgC, hipStream_t s) {
+                                  uint16_t* tab, int mode, int lgC, hipStream_t s, uint32_t cus) {
   switch (lgC) {
-    case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
 #if DLSM_PROBE_P13_HALF
     // 512-thread workgroups of two 4,096-key units (two resident per CU)
-    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
 #else
-    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
 #endif
     // 16,384-key chunks bucketed as two 8,192-key units (DLSM_PROBE_UNITS14)
-    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s);
+    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
     default: return hipErrorInvalidValue;
   }
 }

@@ -117,6 +117,19 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx);
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
 void* dlsm_ctx_stream(dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
+/* Run the HBM-bound partition passes of sliced builds and probes (one job
+ * group / one probe round) on `hip_stream`, and the LDS-bound slice and
+ * unpermute passes on the context stream; events order the two, and a call
+ * is complete when the context stream is.  `cus` sizes the persistent probe
+ * partition grid (the compute units `hip_stream` may use, 0 = all).  With
+ * CU-masked streams (dlsm_stream_create_cu_mask) one node's flush builds and
+ * Get probes share the GPU: partitions on most CUs, build slices on a few.
+ * NULL restores one stream.  Scheduling only: results never depend on it. */
+int dlsm_ctx_set_partition_stream(dlsm_ctx* ctx, void* hip_stream, uint32_t cus);
+/* A hipStream_t restricted to the compute units whose bits are set in
+ * mask[0..words) (bit i of word w = CU 32w + i; hipExtStreamCreateWithCUMask). */
+int dlsm_stream_create_cu_mask(int device, const uint32_t* mask, uint32_t words, void** out);
+int dlsm_stream_destroy(void* hip_stream);
 /* Pre-size the device workspace so later calls never allocate (graph capture). */
 int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs);
 /* Workspace statistics: device allocations the context has made so far
