@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--cosched", type=int, default=0,
                     help="co-schedule build and probe on CU-masked streams: the build's slice pass on this "
                          "many CUs per XCD (1..4), every partition pass on the other CUs (0 = off)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="1: capture one step (build + probe launches) in a HIP graph and replay it")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -180,29 +182,49 @@ def main():
         step()
     ctx.sync()
     ctx_b.sync()
+    graph = None
+    if args.graph and not overlap:
+        # the step's launches captured once (the warm-up sized every
+        # workspace, so the capture allocates nothing and uploads nothing)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+            step()
+        graph.replay()
+        stream.synchronize()
 
     # ---- timed region ----------------------------------------------------
+    dev_events = DeviceEvent.available() and os.environ.get("DLSM_BENCH_TORCH_EVENTS", "0") != "1"
+
     def ev():
-        return torch.cuda.Event(enable_timing=True)
+        return DeviceEvent() if dev_events else torch.cuda.Event(enable_timing=True)
 
     evs = [(ev(), ev(), ev(), ev()) for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    pass_events = os.environ.get("DLSM_BENCH_NO_PASS_EVENTS", "0") != "1" and graph is None
     for i in range(args.steps):
-        evs[i][0].record(stream_b)
+        if graph is not None:
+            graph.replay()
+            continue
+        if pass_events:
+            evs[i][0].record(stream_b)
         if tables:
             ctx_b.full_build_dev(tables, outs, lens, bpk)
-        evs[i][1].record(stream_b)
-        evs[i][2].record(stream)
+        if pass_events:
+            evs[i][1].record(stream_b)
+            evs[i][2].record(stream)
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
-        evs[i][3].record(stream)
+        if pass_events or cosched:
+            evs[i][3].record(stream)
         if cosched:
             # the next build partition starts behind this probe's slice /
             # unpermute passes (co-running with them slows both)
-            stream_b.wait_event(evs[i][3])
+            w = torch.cuda.Event()
+            w.record(stream)
+            stream_b.wait_event(w)
     enqueue_s = time.perf_counter() - t0  # host time to submit the K steps
     stream.synchronize()
     stream_b.synchronize()
@@ -213,7 +235,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = SH.max_over_ranks(elapsed, dist, dev)
-    if cosched:
+    if cosched or not pass_events:
         # co-scheduled passes overlap, so the per-pass times (roofline) come
         # from the same K steps run one pass after another on one stream
         ctx.set_partition_stream(None)
@@ -271,6 +293,7 @@ def main():
             "probe_round_keys": args.probe_round, "probe_serial": args.probe_serial,
             "build_groups": args.build_groups,
             "overlap": overlap,
+            "hip_graph": graph is not None,
             "cosched_build_slice_cus_per_xcd": cosched,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
@@ -280,6 +303,7 @@ def main():
             "traffic": None,
         },
         "host_enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
+        "pass_events": "hipEventReleaseToDevice" if dev_events else "torch.cuda.Event",
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
                   "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
         "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, qk.n) / probe_ms / 1e3, 1),
@@ -318,6 +342,55 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+class DeviceEvent:
+    """A HIP timing event recorded with a device-scope release
+    (hipEventReleaseToDevice).  torch.cuda.Event records with the default
+    system-scope release, which writes back and invalidates the L2 at every
+    record: 11 us of idle GPU per record in a kernel trace of the timed loop,
+    two records between passes."""
+    _hip = None
+    FLAGS = 0x40000000  # hipEventReleaseToDevice (hip_runtime_api.h)
+
+    @classmethod
+    def available(cls) -> bool:
+        if cls._hip is None:
+            import ctypes as C
+
+            try:  # the runtime torch and libdlsm_bloom already share (never a second copy)
+                h = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD)
+                h.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
+                h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
+                h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
+                h.hipEventDestroy.argtypes = [C.c_void_p]
+                cls._hip = h
+            except (OSError, AttributeError):
+                cls._hip = False
+        return bool(cls._hip)
+
+    def __init__(self):
+        import ctypes as C
+
+        self.h = C.c_void_p()
+        if self._hip.hipEventCreateWithFlags(C.byref(self.h), self.FLAGS) != 0:
+            raise RuntimeError("hipEventCreateWithFlags failed")
+
+    def record(self, stream):
+        if self._hip.hipEventRecord(self.h, stream.cuda_stream) != 0:
+            raise RuntimeError("hipEventRecord failed")
+
+    def elapsed_time(self, end) -> float:
+        import ctypes as C
+
+        ms = C.c_float()
+        if self._hip.hipEventElapsedTime(C.byref(ms), self.h, end.h) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return float(ms.value)
+
+    def __del__(self):
+        if getattr(self, "h", None) and self._hip:
+            self._hip.hipEventDestroy(self.h)
 
 
 def load_traffic(path, config, dominant):
