@@ -193,17 +193,15 @@ def main():
         stream.synchronize()
 
     # ---- timed region ----------------------------------------------------
-    dev_events = DeviceEvent.available() and os.environ.get("DLSM_BENCH_TORCH_EVENTS", "0") != "1"
-
     def ev():
-        return DeviceEvent() if dev_events else torch.cuda.Event(enable_timing=True)
+        return torch.cuda.Event(enable_timing=True)
 
     evs = [(ev(), ev(), ev(), ev()) for _ in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pass_events = os.environ.get("DLSM_BENCH_NO_PASS_EVENTS", "0") != "1" and graph is None
+    pass_events = graph is None
     for i in range(args.steps):
         if graph is not None:
             graph.replay()
@@ -303,7 +301,6 @@ def main():
             "traffic": None,
         },
         "host_enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
-        "pass_events": "hipEventReleaseToDevice" if dev_events else "torch.cuda.Event",
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
                   "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
         "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, qk.n) / probe_ms / 1e3, 1),
@@ -342,55 +339,6 @@ def main():
     if dist:
         dist.barrier()
         dist.destroy_process_group()
-
-
-class DeviceEvent:
-    """A HIP timing event recorded with a device-scope release
-    (hipEventReleaseToDevice).  torch.cuda.Event records with the default
-    system-scope release, which writes back and invalidates the L2 at every
-    record: 11 us of idle GPU per record in a kernel trace of the timed loop,
-    two records between passes."""
-    _hip = None
-    FLAGS = 0x40000000  # hipEventReleaseToDevice (hip_runtime_api.h)
-
-    @classmethod
-    def available(cls) -> bool:
-        if cls._hip is None:
-            import ctypes as C
-
-            try:  # the runtime torch and libdlsm_bloom already share (never a second copy)
-                h = C.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD)
-                h.hipEventCreateWithFlags.argtypes = [C.POINTER(C.c_void_p), C.c_uint]
-                h.hipEventRecord.argtypes = [C.c_void_p, C.c_void_p]
-                h.hipEventElapsedTime.argtypes = [C.POINTER(C.c_float), C.c_void_p, C.c_void_p]
-                h.hipEventDestroy.argtypes = [C.c_void_p]
-                cls._hip = h
-            except (OSError, AttributeError):
-                cls._hip = False
-        return bool(cls._hip)
-
-    def __init__(self):
-        import ctypes as C
-
-        self.h = C.c_void_p()
-        if self._hip.hipEventCreateWithFlags(C.byref(self.h), self.FLAGS) != 0:
-            raise RuntimeError("hipEventCreateWithFlags failed")
-
-    def record(self, stream):
-        if self._hip.hipEventRecord(self.h, stream.cuda_stream) != 0:
-            raise RuntimeError("hipEventRecord failed")
-
-    def elapsed_time(self, end) -> float:
-        import ctypes as C
-
-        ms = C.c_float()
-        if self._hip.hipEventElapsedTime(C.byref(ms), self.h, end.h) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return float(ms.value)
-
-    def __del__(self):
-        if getattr(self, "h", None) and self._hip:
-            self._hip.hipEventDestroy(self.h)
 
 
 def load_traffic(path, config, dominant):
