@@ -117,8 +117,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx);
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
 void* dlsm_ctx_stream(dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
-/* Run the HBM-bound partition passes of sliced builds and probes (one job
- * group / one probe round) on `hip_stream`, and the LDS-bound slice and
+/* Run the HBM-bound partition passes of sliced builds (one job group) and of
+ * single-group probes (one round) on `hip_stream`, and the LDS-bound slice and
  * unpermute passes on the context stream; events order the two, and a call
  * is complete when the context stream is.  `cus` sizes the persistent probe
  * partition grid (the compute units `hip_stream` may use, 0 = all).  With

@@ -10,16 +10,6 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_cu_subset_is_balanced_under_both_numberings():
-    import dlsm_amd
-
-    for per in (1, 2, 4):
-        s = dlsm_amd.cu_subset(per)
-        assert len(s) == 8 * per and len(set(s)) == len(s)
-        assert all(sum(1 for i in s if i // 32 == x) == per for x in range(8))
-        assert all(sum(1 for i in s if i % 8 == x) == per for x in range(8))
-
-
 @pytest.mark.parametrize("per_xcd", [1, 4])
 def test_cosched_steps_match_oracle(orc, per_xcd):
     import torch

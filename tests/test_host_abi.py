@@ -131,3 +131,15 @@ def test_slice_kernels_use_no_scratch(tmp_path):
     slices = {k: v for k, v in usage.items() if "slice_kernel" in k}
     assert len(slices) >= 6, sorted(usage)
     assert all(v == 0 for v in slices.values()), slices
+
+
+def test_cu_subset_is_balanced_under_both_numberings():
+    """CU-masked streams (bench --cosched) take the same CUs from every XCD
+    whichever way the mask numbers them."""
+    import dlsm_amd
+
+    for per in (1, 2, 4):
+        s = dlsm_amd.cu_subset(per)
+        assert len(s) == 8 * per and len(set(s)) == len(s)
+        assert all(sum(1 for i in s if i // 32 == x) == per for x in range(8))
+        assert all(sum(1 for i in s if i % 8 == x) == per for x in range(8))
