@@ -180,6 +180,7 @@ def ref_lib():
         R.ref_full_build.restype = C.c_int64
         R.ref_full_build.argtypes = [cp, u64p, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
         R.ref_full_may_match.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
+        R.ref_full_may_match_any.argtypes = [cp, C.c_size_t, cp, C.c_size_t]
         R.ref_full_probe_many.restype = None
         R.ref_full_probe_many.argtypes = [C.POINTER(C.c_void_p), u64p, C.c_int, cp, C.c_uint64,
                                           C.c_uint32, C.c_void_p]

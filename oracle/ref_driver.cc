@@ -111,6 +111,27 @@ int ref_full_may_match(const char* key, size_t klen, const char* filter, size_t 
   return LegacyBloom::HashMayMatchPrepared(h, k, filter + off, 6) ? 1 : 0;
 }
 
+// FullFilterBlockReader::KeyMayMatch (table/full_filter_block.cc:269-279) for
+// any filter the ctor accepts: the ctor's choice of log2_cache_line_size_
+// (:239-249; the member defaults to 0, full_filter_block.h:87) restated here,
+// the probe itself the reference's PrepareHashMayMatch / HashMayMatchPrepared.
+// Returns -1 where the ctor exit(1)s.
+int ref_full_may_match_any(const char* key, size_t klen, const char* filter, size_t flen) {
+  const uint32_t len_with_meta = (uint32_t)flen;
+  if (len_with_meta <= 5) return -1;
+  const int k = static_cast<int>(filter[len_with_meta - 5]);  // signed char (x86), as :209-210
+  if (k < 1) return -1;
+  const uint32_t len = len_with_meta - 5;
+  const uint32_t L = enc_dec32(filter + len_with_meta - 4);
+  int lg = 0;
+  if (L * 64u == len) lg = 6;
+  else if (L == 0 || len % L != 0) return -1;
+  const uint32_t h = TimberSaw::BloomHash(Slice(key, klen));
+  uint32_t off;
+  LegacyBloom::PrepareHashMayMatch(h, L, filter, &off, lg);
+  return LegacyBloom::HashMayMatchPrepared(h, k, filter + off, lg) ? 1 : 0;
+}
+
 // Batch form of the reference reader (the reference has no MultiGet): for key
 // i and filter f, ref_full_may_match -- BloomHash recomputed per filter, as
 // every FullFilterBlockReader::KeyMayMatch call does.  mask[i] bit f.

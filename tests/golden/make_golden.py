@@ -235,6 +235,23 @@ def main():
             k = dbkey(v)
             ans.append(R().ref_full_may_match(k, 20, f, len(f)))
         probe["answers"].append(hx(bytes(ans)))
+    # the reader ctor's two accepted layouts (full_filter_block.cc:239-249):
+    # num_lines * 64 == len (log2 line 6) and len % num_lines == 0 (log2 line
+    # left at 0), random filter bodies, through the reference's probe
+    rng = random.Random(20261017)
+    branches = []
+    for L, line_bytes, k in [(3, 32, 6), (5, 8, 4), (1, 7, 2), (7, 128, 6), (2, 1, 1), (9, 64, 6)]:
+        body = bytes(rng.randrange(256) for _ in range(L * line_bytes))
+        fb = body + bytes([k]) + L.to_bytes(4, "little")
+        ans = bytearray()
+        for v in range(5_000):
+            kk = dbkey(v)
+            r = R().ref_full_may_match_any(kk, 20, fb, len(fb))
+            assert r in (0, 1)
+            ans.append(r)
+        branches.append({"num_lines": L, "line_bytes": line_bytes, "k": k, "filter": hx(fb),
+                         "answers": hx(bytes(ans))})
+    probe["reader_branches"] = {"queries": {"first": 0, "step": 1, "n": 5_000}, "cases": branches}
     with open(os.path.join(HERE, "probe.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py (reference bloom_impl.h HashMayMatch)",
                    **probe}, f, indent=0)

@@ -408,6 +408,26 @@ def test_full_probe_grouped_sliced(gpu, orc, shape):
     fs.close()
 
 
+def test_full_probe_reader_branches_golden(gpu, golden, orc):
+    """The reader ctor's two accepted layouts (log2 line 6 and the
+    len % num_lines == 0 branch with log2 line 0), against answers of the
+    compiled reference (tests/golden/probe.json), filter by filter and all six
+    in one set (the set mixes line counts, so it is probed group by group)."""
+    import dlsm_amd
+
+    g = golden["probe"]["reader_branches"]
+    q = g["queries"]
+    keys = orc.dbbench_keys(q["first"], q["step"], q["n"])
+    filters = [bytes.fromhex(c["filter"]) for c in g["cases"]]
+    wants = [np.frombuffer(bytes.fromhex(c["answers"]), dtype=np.uint8) for c in g["cases"]]
+    for fb, want in zip(filters, wants):
+        got = gpu.full_probe(gpu.filterset([fb]), dlsm_amd.Keys(keys, q["n"], 20))
+        assert np.array_equal(got & 1, want)
+    got = gpu.full_probe(gpu.filterset(filters), dlsm_amd.Keys(keys, q["n"], 20))
+    for f, want in enumerate(wants):
+        assert np.array_equal((got >> f) & 1, want), f
+
+
 def test_full_probe_log2_zero_branch(gpu, orc):
     """A filter whose num_lines*64 != len but len % num_lines == 0: the reference
     probes it with log2_cache_line_size_ == 0 (full_filter_block.h:85)."""
