@@ -1551,8 +1551,23 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
     d.largest_trailer = F.largest_trailer;
     d.f = FilterDev{};
   }
+  // 16-byte big-endian key prefixes (VersionDev::pre_small / pre_large)
+  std::vector<ulonglong2> pre(2 * static_cast<size_t>(n_files));
+  auto be_prefix = [](const uint8_t* p, uint64_t n) {
+    ulonglong2 r{0, 0};
+    for (uint64_t i = 0; i < 16 && i < n; i++) {
+      if (i < 8) r.x |= static_cast<uint64_t>(p[i]) << (56 - 8 * i);
+      else r.y |= static_cast<uint64_t>(p[i]) << (56 - 8 * (i - 8));
+    }
+    return r;
+  };
+  for (int j = 0; j < n_files; j++) {
+    pre[j] = be_prefix(keys.data() + h[j].smallest_off, h[j].smallest_len);
+    pre[n_files + j] = be_prefix(keys.data() + h[j].largest_off, h[j].largest_len);
+  }
+  const uint64_t pre_bytes = (sizeof(ulonglong2) * pre.size() + 255) & ~uint64_t(255);
   const uint64_t keys_bytes = (keys.size() + 255) & ~uint64_t(255);
-  uint64_t total = files_bytes + keys_bytes;
+  uint64_t total = files_bytes + pre_bytes + keys_bytes;
   for (int j = 0; j < n_files; j++) {
     const dlsm_version_file& F = files[order[j]];
     if (!F.filter) continue;
@@ -1588,15 +1603,20 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
   }
   if (e == hipSuccess && n_files)
     e = hipMemcpyAsync(ver->mem, h.data(), sizeof(VFileDev) * n_files, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && n_files)
+    e = hipMemcpyAsync(ver->mem + files_bytes, pre.data(), sizeof(ulonglong2) * pre.size(),
+                       hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !keys.empty())
-    e = hipMemcpyAsync(ver->mem + files_bytes, keys.data(), keys.size(), hipMemcpyHostToDevice, s);
+    e = hipMemcpyAsync(ver->mem + files_bytes + pre_bytes, keys.data(), keys.size(), hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);  // pageable sources: finish before returning
   if (e != hipSuccess) {
     dlsm_version_destroy(ver);
     return from_hip(e);
   }
   ver->v.files = reinterpret_cast<const VFileDev*>(ver->mem);
-  ver->v.keyblob = ver->mem + files_bytes;
+  ver->v.pre_small = reinterpret_cast<const ulonglong2*>(ver->mem + files_bytes);
+  ver->v.pre_large = ver->v.pre_small + n_files;
+  ver->v.keyblob = ver->mem + files_bytes + pre_bytes;
   ver->v.n_l0 = static_cast<uint32_t>(n_l0);
   for (int lv = 0; lv < kNumLevels; lv++) {
     ver->v.lvl_begin[lv] = begin[lv];

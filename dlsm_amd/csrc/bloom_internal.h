@@ -66,6 +66,11 @@ constexpr int kNumLevels = 6;  // config::kNumLevels (db/dbformat.h:26)
 // Files in search order: level-0 newest first, then levels 1.. in key order.
 struct VersionDev {
   const VFileDev* files;
+  // per file (search order) the first 16 bytes of its smallest / largest user
+  // key, zero-padded, as two big-endian u64: comparing them decides the
+  // bytewise order unless they are equal (then the full keys are compared)
+  const ulonglong2* pre_small;
+  const ulonglong2* pre_large;
   const uint8_t* keyblob;
   uint32_t n_l0;
   uint32_t lvl_begin[kNumLevels];

@@ -1647,6 +1647,39 @@ __device__ __forceinline__ int bytewise_cmp(const uint8_t* a, uint64_t an, const
   return an < bn ? -1 : (an > bn ? 1 : 0);
 }
 
+#if DLSM_ABL_VP_NOFILTER  // ablation (timing only, wrong answers): no filter reads
+#define DLSM_VP_MATCH(h, f) (((h) & 1u) != 0u)
+#else
+#define DLSM_VP_MATCH(h, f) full_may_match(h, f)
+#endif
+// The first 16 bytes of a key, zero-padded, as two big-endian u64
+// (VersionDev::pre_small / pre_large).  If two keys' prefixes differ, their
+// order is the bytewise order of the keys: at the first differing byte either
+// both keys have a byte there, or the shorter key has ended (a pad zero) and
+// is a proper prefix of the longer one, which BytewiseComparator also orders
+// first.  Equal prefixes need the full comparison.
+template <int MODE>
+__device__ __forceinline__ ulonglong2 key_prefix(const uint8_t* p, uint64_t len) {
+  ulonglong2 r{0, 0};
+  if (MODE == KM_K20 && len >= 16) {  // 4-byte aligned fixed 20-byte keys
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    r.x = (static_cast<uint64_t>(__builtin_bswap32(w[0])) << 32) | __builtin_bswap32(w[1]);
+    r.y = (static_cast<uint64_t>(__builtin_bswap32(w[2])) << 32) | __builtin_bswap32(w[3]);
+    return r;
+  }
+  for (uint64_t i = 0; i < 16 && i < len; i++) {
+    if (i < 8) r.x |= static_cast<uint64_t>(p[i]) << (56 - 8 * i);
+    else r.y |= static_cast<uint64_t>(p[i]) << (56 - 8 * (i - 8));
+  }
+  return r;
+}
+
+__device__ __forceinline__ int cmp_prefix(const ulonglong2& a, const ulonglong2& b) {
+  if (a.x != b.x) return a.x < b.x ? -1 : 1;
+  if (a.y != b.y) return a.y < b.y ? -1 : 1;
+  return 0;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
                                                                uint64_t* __restrict__ slot_mask,
@@ -1664,35 +1697,48 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
   l = l > kd.suffix ? l - kd.suffix : 0;  // ExtractUserKey
   const uint8_t* uk = kd.bytes + s;
   const uint32_t h = key_hash<MODE>(kd, i);
+  const ulonglong2 q = key_prefix<MODE>(uk, l);
+  // BytewiseComparator order of the lookup user key against a file's
+  // smallest / largest user key (prefixes first, the full keys on a tie)
+  auto vs_small = [&](uint32_t f) {
+    const int r = cmp_prefix(q, v.pre_small[f]);
+    return r ? r : bytewise_cmp(uk, l, v.keyblob + v.files[f].smallest_off, v.files[f].smallest_len);
+  };
+  auto vs_large = [&](uint32_t f) {
+    const int r = cmp_prefix(q, v.pre_large[f]);
+    return r ? r : bytewise_cmp(uk, l, v.keyblob + v.files[f].largest_off, v.files[f].largest_len);
+  };
   // LookupKey(user_key, snapshot): trailer PackSequenceAndType(snapshot, kValueTypeForSeek)
   const uint64_t tnum = (snapshot << 8) | 1u;
   uint64_t m = 0;
   for (uint32_t f = 0; f < v.n_l0; f++) {  // level 0: newest first
-    const VFileDev& F = v.files[f];
-    if (bytewise_cmp(uk, l, v.keyblob + F.smallest_off, F.smallest_len) >= 0 &&
-        bytewise_cmp(uk, l, v.keyblob + F.largest_off, F.largest_len) <= 0 &&
-        (F.f.data == nullptr || full_may_match(h, F.f)))
-      m |= 1ull << f;
+    if (vs_small(f) >= 0 && vs_large(f) <= 0) {
+      const VFileDev& F = v.files[f];
+      if (F.f.data == nullptr || DLSM_VP_MATCH(h, F.f)) m |= 1ull << f;
+    }
   }
   for (int lv = 1; lv < kNumLevels; lv++) {
     const uint32_t nf = v.lvl_count[lv];
     uint32_t pick = 0xffffffffu;
     if (nf) {
-      const VFileDev* fl = v.files + v.lvl_begin[lv];
+      const uint32_t b = v.lvl_begin[lv];
       // FindFile: earliest file whose largest internal key >= the lookup key
       // (right starts at nf-1, so the last file is picked when none is >=)
       uint32_t left = 0, right = nf - 1;
       while (left < right) {
         const uint32_t mid = (left + right) / 2;
-        int r = bytewise_cmp(v.keyblob + fl[mid].largest_off, fl[mid].largest_len, uk, l);
-        if (r == 0) r = fl[mid].largest_trailer > tnum ? -1 : (fl[mid].largest_trailer < tnum ? 1 : 0);
+        int r = -vs_large(b + mid);  // largest vs lookup
+        if (r == 0) {
+          const uint64_t tr = v.files[b + mid].largest_trailer;
+          r = tr > tnum ? -1 : (tr < tnum ? 1 : 0);
+        }
         if (r < 0) left = mid + 1;
         else right = mid;
       }
-      const VFileDev& F = fl[right];
-      if (bytewise_cmp(uk, l, v.keyblob + F.smallest_off, F.smallest_len) >= 0) {
+      if (vs_small(b + right) >= 0) {
         pick = right;
-        if (F.f.data == nullptr || full_may_match(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
+        const VFileDev& F = v.files[b + right];
+        if (F.f.data == nullptr || DLSM_VP_MATCH(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
       }
     }
     if (level_file) level_file[i * (kNumLevels - 1) + (lv - 1)] = pick;

@@ -1,0 +1,116 @@
+"""Batched Get over a version, device-resident: the
+files Version::Get visits for each lookup (db/version_set.cc:273-321) and
+their full-filter answers (table/table.cc:350-358), one
+dlsm_version_probe_dev call per batch.
+
+The version has the shape of db_bench's final state at config 5 (the replay
+of DESIGN.md §7: 5 + 40 + 377 files on levels 1-3 for 100 M keys) plus 4
+level-0 flush files: level files partition the key space [0, V), each file's
+filter holds every key of its range on that level (the key space is spread
+over the levels as 1 : 10 : 100), level-0 files hold 153,846 keys of random
+ranges.  Lookups are uniform over [0, 2V): half of them miss every file.
+Prints one JSON line.
+
+    python scripts/bench_version_probe.py [--lookups 100000000] [--reps 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lookups", type=int, default=100_000_000)
+    ap.add_argument("--space", type=int, default=100_000_000, help="key space V")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--check", type=int, default=200_000, help="lookups checked against the oracle")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+
+    import dlsm_amd
+    from dlsm_amd import VersionFile
+    from dlsm_amd import workload as W
+
+    dev = torch.device("cuda", 0)
+    ctx = dlsm_amd.Context(0)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream)
+    V = args.space
+    key = lambda v: W.dbbench_keys_np(np.array([v], dtype=np.uint64)).tobytes()  # noqa: E731
+
+    def build(values_dev):
+        n = int(values_dev.numel())
+        keys = dlsm_amd.Keys(W.dbbench_keys_torch(values_dev), n, 20)
+        out = torch.zeros(dlsm_amd.full_size(n)[0] + 16, dtype=torch.uint8, device=dev)
+        lens = torch.zeros(1, dtype=torch.uint64, device=dev)
+        ctx.full_build_dev([keys], [out], lens, 10)
+        ctx.sync()
+        return out[: int(lens.cpu()[0])].clone()
+
+    files, host_spec = [], []
+    rng = np.random.default_rng(11)
+    seq = 1 << 30
+    # levels 1..3: nf files partitioning [0, V), keys v = lo + stride * i
+    for level, nf, stride in ((1, 5, 100), (2, 40, 10), (3, 377, 1)):
+        edges = np.linspace(0, V, nf + 1).astype(np.int64)
+        for q in range(nf):
+            lo, hi = int(edges[q]) + (level - 1), int(edges[q + 1]) - 1
+            vals = torch.arange(lo, hi, stride, device=dev, dtype=torch.int64)
+            last = int(vals[-1])
+            files.append(VersionFile(level, 10_000 * level + q, key(lo), key(last), (seq << 8) | 1,
+                                     build(vals)))
+            host_spec.append((level, lo, last, stride))
+            seq -= 1
+    # level 0: 4 flush files of 153,846 keys over random ranges, newest last
+    for j in range(4):
+        lo = int(rng.integers(0, V - 153_846 * 600))
+        step = int(rng.integers(50, 600))
+        vals = torch.arange(lo, lo + 153_846 * step, step, device=dev, dtype=torch.int64)
+        files.append(VersionFile(0, 900_000 + j, key(lo), key(int(vals[-1])), ((seq + 10 + j) << 8) | 1,
+                                 build(vals)))
+    ver = ctx.version(files, on_device=True)
+    filt_bytes = sum(int(f.filter.numel()) for f in files)
+
+    Q = args.lookups
+    qv = torch.from_numpy(rng.integers(0, 2 * V, Q, dtype=np.int64)).to(dev)
+    qk = dlsm_amd.Keys(W.dbbench_keys_torch(qv), Q, 20)
+    mask = torch.zeros(Q, dtype=torch.int64, device=dev)
+    snap = (1 << 56) - 1
+    ctx.version_probe_dev(ver, qk, snap, mask)
+    ctx.sync()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.reps):
+        ctx.version_probe_dev(ver, qk, snap, mask)
+    e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    res = {"what": "version probe (batched Get over a version), device-resident",
+           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt_bytes, "lookups": Q,
+           "ms": round(ms, 3), "mgets_s": round(Q / ms / 1e3, 1)}
+    if args.check:
+        import oracle
+
+        oracle.lib()
+        n = min(args.check, Q)
+        hf = [VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer,
+                          f.filter.cpu().numpy().tobytes()) for f in files]
+        hq = qk.data[: n * 20].cpu().numpy()
+        want, _ = oracle.version_probe(hf, hq, n, snapshot=snap)
+        got = mask[:n].cpu().numpy().astype(np.uint64)
+        res["oracle_checked"] = n
+        res["matches_oracle"] = bool(np.array_equal(got, np.asarray(want, dtype=np.uint64)))
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -156,3 +156,44 @@ def test_gpu_version_rejects_bad_input(gpu):
         gpu.version([VersionFile(1, 1, K(0), K(9), t, b"\x01\x02")])
     with pytest.raises(dlsm_amd.DlsmError):  # level out of range
         gpu.version([VersionFile(6, 1, K(0), K(9), t)])
+
+
+@pytest.mark.gpu
+def test_gpu_version_probe_prefix_ties(gpu):
+    """Keys that the 16-byte prefix comparison cannot order on its own: user
+    keys sharing their first 16 bytes, keys with embedded and trailing zero
+    bytes (b"ab" < b"ab\\0" < b"ab\\0\\0c"), keys shorter than 16 bytes and
+    exact boundary hits, as files' smallest / largest keys and as lookups
+    (no filters: the candidates alone are compared with the oracle)."""
+    import torch
+
+    import dlsm_amd
+
+    t = (1 << 8) | 1
+    P = b"0123456789abcdef"  # a shared 16-byte prefix
+    bounds = [b"", b"\0", b"ab", b"ab\0", b"ab\0\0c", b"ab\x01", P, P + b"\0", P + b"0", P + b"5",
+              P + b"5\0", P + b"9zz", b"0123456789abcdeg", b"\xff" * 3, b"\xff" * 17]
+    bounds = sorted(set(bounds))
+    files = [VersionFile(0, 3, bounds[2], bounds[9], t), VersionFile(0, 7, bounds[5], bounds[12], t)]
+    for q in range(0, len(bounds) - 1, 2):  # level 1: [b_q, b_q+1] ranges, disjoint and ordered
+        files.append(VersionFile(1, 100 + q, bounds[q], bounds[q + 1], ((50 + q) << 8) | 1))
+    files.append(VersionFile(2, 200, bounds[1], bounds[-2], (9 << 8) | 1))
+    probes = set(bounds)
+    for b in bounds:
+        probes |= {b + b"\0", b[:-1], b + b"\xff"}
+    probes = sorted(probes)
+    n = len(probes)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(k) for k in probes])
+    data = np.frombuffer(b"".join(probes) + b"\0" * 16, dtype=np.uint8).copy()
+    for snap in (1 << 40, 60):
+        want, want_lf = oracle.version_probe(files, data, n, snap, offsets=offs)
+        v = gpu.version(files)
+        mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+        lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+        ks = dlsm_amd.Keys(torch.from_numpy(data).cuda(), n, 0, torch.from_numpy(offs).cuda())
+        gpu.version_probe_dev(v, ks, snap, mask, lf)
+        gpu.sync()
+        assert np.array_equal(mask.cpu().numpy().view(np.uint64), want), snap
+        assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf), snap
+        v.close()
