@@ -124,7 +124,9 @@ int dlsm_ctx_sync(dlsm_ctx* ctx);
  * partition grid (the compute units `hip_stream` may use, 0 = all).  With
  * CU-masked streams (dlsm_stream_create_cu_mask) one node's flush builds and
  * Get probes share the GPU: partitions on most CUs, build slices on a few.
- * NULL restores one stream.  Scheduling only: results never depend on it. */
+ * NULL restores one stream.  Scheduling only: results never depend on it.
+ * The stream must outlive the context (dlsm_ctx_destroy synchronises it) or
+ * be detached with NULL first. */
 int dlsm_ctx_set_partition_stream(dlsm_ctx* ctx, void* hip_stream, uint32_t cus);
 /* A hipStream_t restricted to the compute units whose bits are set in
  * mask[0..words) (bit i of word w = CU 32w + i; hipExtStreamCreateWithCUMask). */
