@@ -459,7 +459,7 @@ int dlsm_stream_create_cu_mask(int device, const uint32_t* mask, uint32_t words,
   if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) return DLSM_E_DEVICE;
   DeviceGuard g(device);
   hipStream_t st = nullptr;
-  DLSM_TRY(hipExtStreamCreateWithCUMask(&st, words * 32u, mask));
+  DLSM_TRY(hipExtStreamCreateWithCUMask(&st, words, mask));  // size in uint32 elements
   *out = st;
   return DLSM_OK;
 }
