@@ -23,6 +23,7 @@ DLSM_E_CAPACITY = -2
 DLSM_E_CORRUPT = -3
 DLSM_E_DEVICE = -4
 DLSM_E_NOMEM = -5
+DLSM_E_BUSY = -6
 
 
 class dlsm_keyset(C.Structure):
@@ -74,10 +75,13 @@ SIGNATURES = [
     ("dlsm_ctx_stats", C.c_int, [_VP, _U64P, _U64P]),
     ("dlsm_ctx_set_path", C.c_int, [_VP, C.c_int]),
     ("dlsm_ctx_set_option", C.c_int, [_VP, C.c_int, C.c_uint64]),
+    ("dlsm_ctx_get_option", C.c_int, [_VP, C.c_int, _U64P]),
     ("dlsm_host_register", C.c_int, [_VP, C.c_size_t]),
     ("dlsm_host_unregister", C.c_int, [_VP]),
     ("dlsm_host_alloc", C.c_int, [C.c_size_t, C.POINTER(_VP)]),
     ("dlsm_host_free", C.c_int, [_VP]),
+    ("dlsm_ctx_host_buffer_claim", C.c_int, [_VP, _VP]),
+    ("dlsm_ctx_host_buffer_release", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_host_buffer", C.c_int, [_VP, C.c_uint64, C.c_uint64, C.POINTER(_VP), _U64P]),
     ("dlsm_bloom_full_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -140,6 +141,7 @@ struct dlsm_ctx {
   // page-locked host staging lent to the context's (single) builder
   void* host_buf = nullptr;
   uint64_t host_cap = 0;
+  std::atomic<const void*> host_owner{nullptr};
 };
 
 // A stacked image of the filters of one mask byte that share a line count
@@ -318,6 +320,7 @@ const char* dlsm_strerror(int status) {
     case DLSM_E_CORRUPT: return "corrupt bloom filter";
     case DLSM_E_DEVICE: return "HIP device error";
     case DLSM_E_NOMEM: return "device out of memory";
+    case DLSM_E_BUSY: return "host staging buffer held by another user";
     default: return "unknown status";
   }
 }
@@ -516,6 +519,20 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
   }
 }
 
+int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
+  if (!ctx || !value) return DLSM_E_ARG;
+  switch (option) {
+    case DLSM_OPT_PATH: *value = static_cast<uint64_t>(ctx->path); return DLSM_OK;
+    case DLSM_OPT_PROBE_ROUND_KEYS: *value = ctx->probe_round; return DLSM_OK;
+    case DLSM_OPT_BUILD_GROUPS: *value = static_cast<uint64_t>(ctx->build_groups); return DLSM_OK;
+    case DLSM_OPT_PROBE_CHUNK_LG: *value = static_cast<uint64_t>(ctx->probe_lgc); return DLSM_OK;
+    case DLSM_OPT_PROBE_SLICE_LG: *value = static_cast<uint64_t>(ctx->probe_lgr); return DLSM_OK;
+    case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
+    case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
+    default: return DLSM_E_ARG;
+  }
+}
+
 int dlsm_ctx_reserve(dlsm_ctx* ctx, uint64_t max_keys, uint32_t max_jobs) {
   if (!ctx) return DLSM_E_ARG;
   DeviceGuard g(ctx->device);
@@ -565,6 +582,19 @@ int dlsm_host_unregister(void* p) {
   if (!p) return DLSM_E_ARG;
   DLSM_TRY(hipHostUnregister(p));
   return DLSM_OK;
+}
+
+int dlsm_ctx_host_buffer_claim(dlsm_ctx* ctx, const void* owner) {
+  if (!ctx || !owner) return DLSM_E_ARG;
+  const void* cur = nullptr;
+  if (ctx->host_owner.compare_exchange_strong(cur, owner) || cur == owner) return DLSM_OK;
+  return DLSM_E_BUSY;
+}
+
+int dlsm_ctx_host_buffer_release(dlsm_ctx* ctx, const void* owner) {
+  if (!ctx || !owner) return DLSM_E_ARG;
+  const void* cur = owner;
+  return ctx->host_owner.compare_exchange_strong(cur, nullptr) ? DLSM_OK : DLSM_E_ARG;
 }
 
 int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes, void** out,
@@ -662,10 +692,8 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
     d.reserved = 0;
     starts[j] = chunk;
     starts[n_jobs + j] = slice;
-    // chunk regions of kBuildRegion entries (padded buckets), or the keys
-    // back to back, 16-element aligned: 16-byte stores
-    entry += DLSM_BUILD_UNITS ? static_cast<uint64_t>(d.n_chunks) * kBuildRegion
-                              : (b.keys.n + 15) & ~uint64_t(15);
+    // chunk regions of kBuildRegion entries (buckets padded to 16-byte units)
+    entry += static_cast<uint64_t>(d.n_chunks) * kBuildRegion;
     chunk += d.n_chunks;
     slice += d.n_slices;
     tabw += static_cast<uint64_t>(d.n_slices + 1) * d.n_chunks;

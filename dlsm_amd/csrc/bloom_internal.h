@@ -94,14 +94,12 @@ constexpr uint32_t kBuildSliceCUs = 256;  // MI355X CUs: the build's slice-count
 #define DLSM_BUILD_CHUNK 4096
 #endif
 constexpr int kBuildChunk = DLSM_BUILD_CHUNK;  // keys per partition chunk (build)
-// DLSM_BUILD_UNITS: the build partition pads every slice bucket of a chunk to
-// whole 16-byte units (pad entries have bit 31 set), so the slice pass loads
-// 4 entries per lane per load; each chunk then owns a region of kBuildRegion
-// entries (its keys plus up to 3 pads per bucket).
-#ifndef DLSM_BUILD_UNITS
-#define DLSM_BUILD_UNITS 1  // r02: build slice 65.7 -> 50.8 us, build 0.176 -> 0.165 ms (profiles/r02_ab_units_pred.txt)
-#endif
-constexpr uint32_t kBuildRegion = DLSM_BUILD_UNITS ? kBuildChunk + 4u * kMaxSlices : kBuildChunk;
+// The build partition pads every slice bucket of a chunk to whole 16-byte
+// units (pad entries have bit 31 set), so the slice pass loads 4 entries per
+// lane per load; each chunk owns a region of kBuildRegion entries (its keys
+// plus up to 3 pads per bucket).  r02: build slice 65.7 -> 50.8 us
+// (profiles/r02_ab_units_pred.txt).
+constexpr uint32_t kBuildRegion = kBuildChunk + 4u * kMaxSlices;
 constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
 // u32 entries (and answer bytes) per probe chunk region: C keys plus up to 3
 // padding entries per slice bucket (buckets are padded to 16-byte units).

@@ -197,21 +197,6 @@ __device__ __forceinline__ void lds_add_hash_k(uint32_t* line, uint32_t h) {
   }
 }
 
-#if DLSM_ABL_BUILD_NOCF
-// Ablation (timing only, wrong filters): the same k LDS ORs with lane l's
-// words all in bank l & 31 -- the build slice pass without bank conflicts.
-template <int K>
-__device__ __forceinline__ void lds_add_hash_nocf(uint32_t* sl, uint32_t h) {
-  const uint32_t delta = bloom_delta(h);
-#pragma unroll
-  for (int i = 0; i < K; i++) {
-    const uint32_t bp = h & 511u;
-    atomicOr(&sl[((bp >> 5) << 5) | (threadIdx.x & 31u)], 1u << (bp & 31u));
-    h += delta;
-  }
-}
-#endif
-
 // Filter trailer (full_filter_block.cc:133-135): k byte + Fixed32 num_lines.
 __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
   uint8_t* t = out + static_cast<uint64_t>(L) * 64u;
@@ -462,45 +447,9 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // its flat start `excl` inside the group (wave prefix scan of the counts) and
 // dv = l*CHUNK + off - excl, where off is the segment's offset inside chunk
 // l's region, so flat entry e of segment l sits at in-group offset e + dv.
-// `nz` is the wave mask of non-empty segments.  A window [w, w+64) starts in
-// the last non-empty segment with excl <= w and crosses into every non-empty
-// segment that starts inside it; those boundaries are wave-uniform (ballot,
-// s_ff1, readlane), so each lane picks its dv with one compare + select per
-// boundary (about two per window at the bench shapes): no LDS permutes and
-// no per-window scans.  Lanes past T take the window's first entry, so every
-// index stays inside the group.
-template <int U>
-__device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint64_t nz, uint32_t T,
-                                               uint32_t w0, uint32_t (&idx)[U], bool (&ok)[U]) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint32_t w = w0 + u * kWin;
-    if (w >= T) {  // wave-uniform; never for u = 0 (next() only runs with e0 < T)
-      ok[u] = false;
-      idx[u] = u > 0 ? idx[0] : lane;  // re-reads window 0's units: see walk_segments
-      continue;
-    }
-    const uint64_t below = uniform64(__ballot(excl <= w) & nz);
-    uint32_t d = static_cast<uint32_t>(
-        __builtin_amdgcn_readlane(static_cast<int>(dv), 63 - __builtin_clzll(below)));
-    uint64_t m = uniform64(__ballot(excl > w && excl < w + kWin) & nz);
-    while (m) {
-      const int l = __builtin_ctzll(m);
-      m &= m - 1;
-      const uint32_t st = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(excl), l));
-      const uint32_t dl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(dv), l));
-      if (w + lane >= st) d = dl;
-    }
-    const uint32_t id = w + lane + d;
-    const uint32_t id0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0));
-    ok[u] = w + lane < T;
-    idx[u] = ok[u] ? id : id0;
-  }
-}
-
-// LDS-assisted form of seg_locate_win (DLSM_WALK_LDS, the default): no
-// per-boundary scalar loop.  At group setup the non-empty segments' dv are
+// `nz` is the wave mask of non-empty segments.  Lanes past T take the
+// window's first entry, so every index stays inside the group.
+// Located with LDS help, no per-boundary scalar loop.  At group setup the non-empty segments' dv are
 // compacted into the wave's LDS list dvc[0..); per window, every segment
 // that starts inside the window marks its start lane in the wave's 64-flag
 // array, one ballot of the flags gives the window's boundary mask B, and lane
@@ -513,23 +462,11 @@ __device__ __forceinline__ void seg_locate_win(uint32_t excl, uint32_t dv, uint6
 // wavefront-scope fence between the flag stores and the flag load keeps the
 // compiler from treating the exchange as single-thread memory.  The pointers
 // carry the LDS address space (a generic pointer would become flat accesses).
-#ifndef DLSM_WALK_LDS
-#define DLSM_WALK_LDS 1
-#endif
-#ifndef DLSM_WALK_PROLOGUE_WAIT
-#define DLSM_WALK_PROLOGUE_WAIT 1
-#endif
-#ifndef DLSM_PROBE_UNCOND_STORE
-#define DLSM_PROBE_UNCOND_STORE 1
-#endif
-#ifndef DLSM_WALK_SET
-#define DLSM_WALK_SET 1
-#endif
 constexpr int kWalkScratch = 192;  // u32 per wave: 64 x min(U, 2) flags + 64 compacted dv
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // flags per wave for a walk of U windows per set (seg_locate_set_lds for U <= 2)
 template <int U>
-constexpr int walk_flags() { return (DLSM_WALK_SET && U <= 2) ? 64 * U : 64; }
+constexpr int walk_flags() { return U <= 2 ? 64 * U : 64; }
 
 template <int U>
 __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, uint32_t T, uint32_t w0,
@@ -562,7 +499,7 @@ __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, u
   }
 }
 
-// Set-wide form (DLSM_WALK_SET, U <= 2): the flags of the whole window set
+// Set-wide form (U <= 2): the flags of the whole window set
 // are marked at once and stamped with the set's tag instead of being cleared
 // (a wave-private running count, the array initialised to ~0 at the walk's
 // start), so a set costs one flag store, one fence, then per window one flag
@@ -624,7 +561,7 @@ struct SegWalk {
   uint32_t gs;        // chunks per group (<= 64; lanes >= gs hold empty segments)
   uint32_t g;         // current group (first chunk)
   uint32_t e0;        // next window start in the current group
-  lds_u32* scr;       // the wave's kWalkScratch u32 of LDS (DLSM_WALK_LDS)
+  lds_u32* scr;       // the wave's kWalkScratch u32 of LDS
   uint32_t tag;       // window sets located so far (seg_locate_set_lds stamps)
   static constexpr int kFlags = walk_flags<U>();
   uint32_t excl, dv, T;
@@ -650,13 +587,11 @@ struct SegWalk {
     dv = lane * CHUNK + a0 - excl;
     nz = uniform64(__ballot(cnt != 0u));
     e0 = 0;
-#if DLSM_WALK_LDS
     if (cnt != 0u) {  // compact the non-empty segments' dv (ordered by lane = by excl)
       const uint32_t k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(nz >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(nz), 0u));
       scr[kFlags + k] = dv;
     }
-#endif
   }
   // The next group's rows are prefetched unconditionally (load_rows clamps
   // past-the-end groups to the last chunk): a prefetch under a branch makes
@@ -665,13 +600,11 @@ struct SegWalk {
   __device__ __forceinline__ bool start(uint32_t g_first) {
     g = g_first;
     if (g >= g_end) return false;
-#if DLSM_WALK_LDS
-    if constexpr (kFlags > 64 || (DLSM_WALK_SET && U <= 2)) {
+    if constexpr (U <= 2) {
 #pragma unroll
       for (int u = 0; u < kFlags / 64; u++) scr[u * 64 + (threadIdx.x & 63)] = ~0u;
       tag = 0;
     }
-#endif
     const uint32_t row = load_rows(g);
     nrow = load_rows(g + g_step);
     setup(row);
@@ -697,31 +630,18 @@ struct SegWalk {
         setup(row2);
       }
     }
-#if DLSM_WALK_LDS
-    if constexpr (DLSM_WALK_SET && U <= 2)
+    if constexpr (U <= 2)
       seg_locate_set_lds<U>(excl, nz, T, e0, tag++, scr, scr + kFlags, idx, ok);
     else
       seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + kFlags, idx, ok);
-#else
-    seg_locate_win<U>(excl, dv, nz, T, e0, idx, ok);
-#endif
     e0 += kWin * U;
     gset = g;
     return true;
   }
   __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
     const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
-#if DLSM_ABL_NOLOAD  // ablation (timing only, wrong answers): the walk without its entry loads
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      if constexpr (sizeof(E) == 16) hv[u] = make_uint4(idx[u] * 0x9e3779b9u, idx[u], idx[u] << 7, idx[u] ^ gset);
-      else hv[u] = idx[u] * 0x9e3779b9u;
-    }
-    (void)gent;
-#else
 #pragma unroll
     for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
-#endif
   }
 };
 
@@ -746,14 +666,12 @@ __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowle
   WinSet<U, CHUNK, E> A, B;
   if (!w.next(A.idx, A.ok, A.g)) return;
   w.fetch(A.idx, A.g, A.hv);
-#if DLSM_WALK_PROLOGUE_WAIT
   // The first set's loads land in A's registers, which the loop refills by
   // copies: left pending into the loop, the compiler's wait for them merges
   // with the loop's state into an s_waitcnt vmcnt(0) placed right after every
   // iteration's prefetch -- each set's loads were waited on where they were
   // issued.  Waiting once here keeps the loop's waits at the copies.
   __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
-#endif
   bool haveB = false;
   if constexpr (DEPTH == 2) {
     haveB = w.next(B.idx, B.ok, B.g);
@@ -851,9 +769,7 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
   constexpr int TVB = TKV > RV ? TKV : RV;
   __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
   __shared__ uint32_t hist[kMaxSlices + 1];
-#if DLSM_BUILD_UNITS
   __shared__ uint8_t npad[kMaxSlices + 1];
-#endif
   __shared__ uint32_t lastw[PER * (kPartBlock / 64)];
   __shared__ uint32_t wsum[kPartBlock / 64];
   __shared__ int sj;
@@ -899,38 +815,29 @@ __global__ __launch_bounds__(kPartBlock) void full_partition_kernel(
     }
   }
   __syncthreads();
-#if DLSM_BUILD_UNITS
   for (uint32_t b = tid; b < S; b += kPartBlock) {  // pad every bucket to whole 16-byte units
     const uint32_t pad = (0u - hist[b]) & 3u;
     npad[b] = static_cast<uint8_t>(pad);
     hist[b] += pad;
   }
   __syncthreads();
-#endif
   const uint32_t total = block_excl_scan_lds<kPartBlock>(hist, static_cast<int>(S + 1), wsum);
   for (uint32_t b = tid; b <= S; b += kPartBlock)
     tab[J.tab0 + static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);  // free since hash_chunk's last barrier
-#if DLSM_BUILD_UNITS
   for (uint32_t b = tid; b < S; b += kPartBlock) {
     const uint32_t end = hist[b + 1], np = npad[b];
     if (np > 0) stage[end - 1] = kBuildPadEntry;
     if (np > 1) stage[end - 2] = kBuildPadEntry;
     if (np > 2) stage[end - 3] = kBuildPadEntry;
   }
-#endif
 #pragma unroll
   for (int r = 0; r < PER; r++) {
     const uint32_t i = r * kPartBlock + tid;
     if (i < nk) stage[hist[code[r] & 511u] + (code[r] >> 9)] = h[r];
   }
   __syncthreads();
-#if DLSM_BUILD_UNITS
   store_chunk_u32<kPartBlock>(entries + J.entry0 + static_cast<uint64_t>(c) * kBuildRegion, stage, total);
-#else
-  (void)total;
-  store_chunk_u32<kPartBlock>(entries + J.entry0 + first, stage, nk);
-#endif
 }
 
 // Sum of a job's per-chunk distinct counts (every thread gets the total).
@@ -996,7 +903,6 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
     const uint16_t* __restrict__ tab, uint32_t block0) {
   constexpr uint32_t R = 1u << LGR;
-  [[maybe_unused]] constexpr int U = kWalkU;
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
@@ -1032,7 +938,6 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       const uint32_t gs = nC >= 256u ? (DLSM_BUILD_GS ? min(64u, max(1u, (nC + NW - 1) / NW))
                                                         : 64u)
                                      : max(1u, (nC + NW - 1) / NW);
-#if DLSM_BUILD_UNITS
       // 16-byte units of 4 entries per lane per load (padding entries skipped)
       constexpr int U4 = kWalkU / 4;
       walk_segments<U4, kBuildRegion / 4, uint4, DLSM_BUILD_DEPTH>(
@@ -1044,11 +949,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
                 const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
 #pragma unroll
                 for (int j = 0; j < 4; j++)
-#if DLSM_ABL_BUILD_NOCF
-                  if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash_nocf<6>(sl, e4[j]);
-#else
                   if (ok[u] && !(e4[j] & kBuildPadEntry)) lds_add_hash_k<6>(sl + build_entry_off(e4[j]) * 16u, e4[j]);
-#endif
               }
             } else {
 #pragma unroll
@@ -1060,21 +961,6 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
               }
             }
           });
-#else
-      walk_segments<U, kBuildChunk>(
-          tb, J.n_slices + 1, ent, wv * gs, NW * gs, nC, gs, walk_scr + wv * kWalkScratch,
-          [&](const uint32_t (&hv)[U], const uint32_t (&)[U], const bool (&ok)[U], uint32_t) {
-            if (k == 6) {  // bits_per_key 10 (ChooseNumProbes): straight-line probes
-#pragma unroll
-              for (int u = 0; u < U; u++)
-                if (ok[u]) lds_add_hash_k<6>(sl + build_entry_off(hv[u]) * 16u, hv[u]);
-            } else {
-#pragma unroll
-              for (int u = 0; u < U; u++)
-                if (ok[u]) lds_add_hash(sl + build_entry_off(hv[u]) * 16u, hv[u], k);
-            }
-          });
-#endif
     } else {
       // Duplicates lowered the line count below the speculative one: the
       // partition used the wrong modulus (and the entries no longer hold the
@@ -1252,24 +1138,6 @@ __device__ __forceinline__ uint32_t probe_entry_off(uint32_t e) {
   return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
 }
 
-// Phase timestamps of the persistent probe partition (diagnostic builds only,
-// make variant TAG=stamps VFLAGS=-DDLSM_STAMPS=1; scripts/partition_stamps.py):
-// wave 0 of workgroup b stamps s_memtime at the phase ends of its chunk
-// iteration it.
-#if DLSM_STAMPS
-constexpr int kStampWGs = 1024, kStampIters = 64, kStampPhases = 8;
-__device__ uint64_t g_stamps[kStampWGs * kStampIters * kStampPhases];
-#define DLSM_STAMP(ph, it)                                                                     \
-  do {                                                                                         \
-    if (threadIdx.x == 0 && blockIdx.x < kStampWGs && (it) < kStampIters)                      \
-      g_stamps[(blockIdx.x * kStampIters + (it)) * kStampPhases + (ph)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define DLSM_STAMP(ph, it) \
-  do {                     \
-  } while (0)
-#endif
-
 // f(b) for every bucket b < n (n <= kMaxSlices + 1): one bucket per thread
 // when the workgroup has enough threads.  A strided loop's per-lane trip
 // count is a loop invariant the persistent partition spilled to scratch, and
@@ -1343,8 +1211,6 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   }
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
   for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
-    [[maybe_unused]] const uint32_t it = (c - blockIdx.x) / gridDim.x;
-    DLSM_STAMP(0, it);
     const uint64_t first = static_cast<uint64_t>(c) * C;
     const uint32_t nk = chunk_keys(c);
     for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
@@ -1359,9 +1225,13 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
         const uint32_t nn = u + 1 < H ? unit_keys(nk, u + 1) : (cn < nC ? unit_keys(chunk_keys(cn), 0) : 0u);
         hash_chunk_k20_pipe<NT, PER, KB>(kd, fu, nku, nf, nn, tile, h, pre);  // ends with a barrier
       } else {
-        hash_chunk<MODE, NT, PER>(kd, fu, nku, tile, h);  // ends with a barrier
+        // K20 / K28 end with a barrier; KM_HASH / GENERIC load straight to
+        // registers, so the bucket counters' zeroing above needs its own
+        if constexpr (MODE == KM_HASH || MODE == KM_GENERIC) {
+          if (u == 0) __syncthreads();
+        }
+        hash_chunk<MODE, NT, PER>(kd, fu, nku, tile, h);
       }
-      DLSM_STAMP(1 + 2 * (u & 1), it);
 #pragma unroll
       for (int r = 0; r < PER; r++) {
         const uint32_t il = r * NT + tid;
@@ -1375,7 +1245,6 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
           if (u + 1 < H) park[i] = h[r];
         }
       }
-      DLSM_STAMP(2 + 2 * (u & 1), it);
     }
     __syncthreads();
     for_buckets<NT>(S, [&](uint32_t b) {  // pad every bucket to whole 16-byte units
@@ -1385,7 +1254,6 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     });
     __syncthreads();
     const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
-    DLSM_STAMP(5, it);
     for_buckets<NT>(S + 1, [&](uint32_t b) {  // one row per chunk
       tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
     });
@@ -1416,7 +1284,6 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
       }
     }
     __syncthreads();
-    DLSM_STAMP(6, it);
     // The next unit's key tiles (issued before the bucketing) are waited for
     // HERE, while only loads are in flight: once the stores below are pending
     // every wait is a full vmcnt(0) that would also wait for their acks.
@@ -1425,7 +1292,6 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     store_chunk_u32<NT, NTS>(entries + static_cast<uint64_t>(c) * CR, stage, total);
     store_chunk_u16<NT, NTS>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
-    DLSM_STAMP(7, it);
   }
 }
 
@@ -1500,9 +1366,6 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
   const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
-#if DLSM_ABL_NOSTORE
-  uint32_t abl_sink = 0;
-#endif
   walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
       tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch,
       [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
@@ -1539,15 +1402,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
             if constexpr (K > 0) {
 #pragma unroll
               for (int q = 0; q < K; q++) {
-#if DLSM_ABL_NOLDS  // ablation (timing only, wrong answers): no LDS probe reads
-                acc &= (base | (x & 511u)) >> 3;
-#elif DLSM_ABL_NOCONFLICT  // ablation (timing only, wrong answers): lane l reads bank l & 31
-                acc &= sl[((x & 511u) << 8) | ((threadIdx.x & 31u) << 2)];
-#elif DLSM_ABL_TRANSPOSED  // ablation (timing only, wrong answers): [bitpos][line] address, random banks
-                acc &= sl[((x & 511u) << 8) | (base >> 9)];
-#else
                 acc &= sl[base | (x & 511u)];
-#endif
                 x += delta;
               }
             } else {
@@ -1567,18 +1422,8 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
         // vmcnt(0) that also waits for these stores' acks (every path must
         // agree on the count).
 #pragma unroll
-        for (int u = 0; u < U; u++)
-#if DLSM_ABL_NOSTORE  // ablation (timing only): no answer stores in the walk (folded into one per lane)
-          abl_sink ^= ans[u] + idx[u];
-#elif DLSM_PROBE_UNCOND_STORE
-          gmask[idx[u]] = ans[u];
-#else
-          if (ok[u]) gmask[idx[u]] = ans[u];
-#endif
+        for (int u = 0; u < U; u++) gmask[idx[u]] = ans[u];
       });
-#if DLSM_ABL_NOSTORE
-  if (abl_sink == 0x12345678u) smask[tid] = 1;
-#endif
 }
 
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
@@ -1647,11 +1492,6 @@ __device__ __forceinline__ int bytewise_cmp(const uint8_t* a, uint64_t an, const
   return an < bn ? -1 : (an > bn ? 1 : 0);
 }
 
-#if DLSM_ABL_VP_NOFILTER  // ablation (timing only, wrong answers): no filter reads
-#define DLSM_VP_MATCH(h, f) (((h) & 1u) != 0u)
-#else
-#define DLSM_VP_MATCH(h, f) full_may_match(h, f)
-#endif
 // The first 16 bytes of a key, zero-padded, as two big-endian u64
 // (VersionDev::pre_small / pre_large).  If two keys' prefixes differ, their
 // order is the bytewise order of the keys: at the first differing byte either
@@ -1714,7 +1554,7 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
   for (uint32_t f = 0; f < v.n_l0; f++) {  // level 0: newest first
     if (vs_small(f) >= 0 && vs_large(f) <= 0) {
       const VFileDev& F = v.files[f];
-      if (F.f.data == nullptr || DLSM_VP_MATCH(h, F.f)) m |= 1ull << f;
+      if (F.f.data == nullptr || full_may_match(h, F.f)) m |= 1ull << f;
     }
   }
   for (int lv = 1; lv < kNumLevels; lv++) {
@@ -1738,7 +1578,7 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
       if (vs_small(b + right) >= 0) {
         pick = right;
         const VFileDev& F = v.files[b + right];
-        if (F.f.data == nullptr || DLSM_VP_MATCH(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
+        if (F.f.data == nullptr || full_may_match(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
       }
     }
     if (level_file) level_file[i * (kNumLevels - 1) + (lv - 1)] = pick;
@@ -2354,12 +2194,3 @@ hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t ma
 }
 
 }  // namespace dlsm
-
-#if DLSM_STAMPS
-// Diagnostic builds only: copy the partition's phase stamps to the host.
-extern "C" int dlsm_debug_stamps(uint64_t* host, uint64_t n) {
-  const uint64_t cap = static_cast<uint64_t>(dlsm::kStampWGs) * dlsm::kStampIters * dlsm::kStampPhases;
-  if (n > cap) n = cap;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dlsm::g_stamps), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
-}
-#endif

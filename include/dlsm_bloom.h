@@ -45,6 +45,7 @@ extern "C" {
 #define DLSM_E_CORRUPT (-3)  /* filter metadata the reference rejects or cannot probe */
 #define DLSM_E_DEVICE (-4)   /* HIP runtime error */
 #define DLSM_E_NOMEM (-5)    /* device allocation failed */
+#define DLSM_E_BUSY (-6)     /* the context's host staging buffer is held by another user */
 
 typedef struct dlsm_ctx dlsm_ctx;             /* one device + one stream + workspace */
 typedef struct dlsm_filterset dlsm_filterset; /* F parsed full filters resident on a device */
@@ -169,6 +170,8 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_BUILD_EXACT 5
 #define DLSM_OPT_PROBE_ROUND_SERIAL 6
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
+/* The current value of an option (so a caller can restore it). */
+int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);
 
 /* Page-lock a host range (e.g. an RDMA-registered FilterChunk slot) so D2H
  * copies land in it directly. */
@@ -178,12 +181,16 @@ int dlsm_host_unregister(void* p);
  * run as DMA at the link rate). */
 int dlsm_host_alloc(size_t len, void** out);
 int dlsm_host_free(void* p);
-/* The context's own page-locked host staging buffer, lent to the builder that
- * uses the context (one at a time: the reference runs one TableBuilder per
- * thread, one context per thread): at least min_bytes; when it has to grow,
- * its first keep_bytes bytes move to the new buffer.  Valid until the next
- * call that grows it or dlsm_ctx_destroy.  Builders created per SSTable reuse
- * it, so key staging allocates nothing after the first table. */
+/* The context's own page-locked host staging buffer, lent to ONE user at a
+ * time (the reference runs one TableBuilder per thread, one context per
+ * thread): claim returns DLSM_OK when the buffer is free or already held by
+ * `owner`, DLSM_E_BUSY when another owner holds it; release gives it back.
+ * dlsm_ctx_host_buffer (for the holder): at least min_bytes; when it has to
+ * grow, its first keep_bytes bytes move to the new buffer.  Valid until the
+ * next call that grows it or dlsm_ctx_destroy.  Builders created per SSTable
+ * reuse it, so key staging allocates nothing after the first table. */
+int dlsm_ctx_host_buffer_claim(dlsm_ctx* ctx, const void* owner);
+int dlsm_ctx_host_buffer_release(dlsm_ctx* ctx, const void* owner);
 int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes, void** out,
                          uint64_t* cap);
 

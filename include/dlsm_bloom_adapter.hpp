@@ -94,22 +94,23 @@ struct FilterSlot {
   size_t length;
 };
 
-// Key staging in the context's page-locked host buffer
-// (dlsm_ctx_host_buffer): AddKey writes the keys where Finish's H2D DMA reads
-// them, and builders created per SSTable reuse the context's buffer.
+// Key staging in page-locked host memory: AddKey writes the keys where
+// Finish's H2D DMA reads them.  The first builder on a context claims the
+// context's own buffer (dlsm_ctx_host_buffer_claim), so builders created one
+// after another per SSTable reuse it and allocate nothing after the first
+// table; a builder that finds it held by another live builder on the same
+// context stages into a private pinned buffer instead of sharing bytes.
 class PinnedBytes {
  public:
   explicit PinnedBytes(dlsm_ctx* ctx) : ctx_(ctx) {}
   PinnedBytes(const PinnedBytes&) = delete;
   PinnedBytes& operator=(const PinnedBytes&) = delete;
+  ~PinnedBytes() {
+    if (shared_) dlsm_ctx_host_buffer_release(ctx_, this);
+    else if (p_) dlsm_host_free(p_);
+  }
   bool append(const char* d, size_t n) {
-    if (size_ + n > cap_) {
-      void* q = nullptr;
-      uint64_t c = 0;
-      if (dlsm_ctx_host_buffer(ctx_, size_ + n, size_, &q, &c) != DLSM_OK) return false;
-      p_ = static_cast<uint8_t*>(q);
-      cap_ = c;
-    }
+    if (size_ + n > cap_ && !grow(size_ + n)) return false;
     memcpy(p_ + size_, d, n);
     size_ += n;
     return true;
@@ -117,11 +118,35 @@ class PinnedBytes {
   void clear() { size_ = 0; }
   const uint8_t* data() const { return p_ ? p_ : reinterpret_cast<const uint8_t*>(""); }
   size_t size() const { return size_; }
+  bool shared() const { return shared_; }
 
  private:
+  bool grow(size_t need) {
+    if (!decided_) {
+      decided_ = true;
+      shared_ = dlsm_ctx_host_buffer_claim(ctx_, this) == DLSM_OK;
+    }
+    void* q = nullptr;
+    if (shared_) {
+      uint64_t c = 0;
+      if (dlsm_ctx_host_buffer(ctx_, need, size_, &q, &c) != DLSM_OK) return false;
+      p_ = static_cast<uint8_t*>(q);
+      cap_ = c;
+      return true;
+    }
+    size_t c = cap_ ? 2 * cap_ : (size_t(1) << 20);
+    if (c < need) c = need;
+    if (dlsm_host_alloc(c, &q) != DLSM_OK) return false;
+    if (size_) memcpy(q, p_, size_);
+    if (p_) dlsm_host_free(p_);
+    p_ = static_cast<uint8_t*>(q);
+    cap_ = c;
+    return true;
+  }
   dlsm_ctx* ctx_;
   uint8_t* p_ = nullptr;
   size_t size_ = 0, cap_ = 0;
+  bool decided_ = false, shared_ = false;
 };
 
 class FullFilterBlockBuilder {
@@ -141,6 +166,7 @@ class FullFilterBlockBuilder {
   // LDS-tiled key loaders) and whether a key repeats its predecessor (then
   // the line count is counted exactly before bucketing: DLSM_OPT_BUILD_EXACT).
   void AddKey(const Slice& key) {
+    if (status_ != DLSM_OK) return;  // staging failed: Finish reports it
     const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
     if (n_ == 0) {
       key_len_ = key.size();
@@ -152,7 +178,10 @@ class FullFilterBlockBuilder {
         for (uint64_t i = 0; i <= n_; i++) offsets_[i] = i * key_len_;
       }
     }
-    if (!keys_.append(key.data(), key.size())) status_ = DLSM_E_NOMEM;
+    if (!keys_.append(key.data(), key.size())) {
+      status_ = DLSM_E_NOMEM;
+      return;
+    }
     if (!uniform_) offsets_.push_back(keys_.size());
     last_len_ = key.size();
     n_++;
@@ -177,25 +206,40 @@ class FullFilterBlockBuilder {
       job.keys.key_len = 0;
     }
     job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
-    job.out_cap = local_mr_->length - static_cast<size_t>(result.data() - static_cast<char*>(local_mr_->addr));
-    if (result.data() < static_cast<char*>(local_mr_->addr) ||
-        result.data() >= static_cast<char*>(local_mr_->addr) + local_mr_->length)
-      job.out_cap = moved_cap_;
+    job.out_cap = output_capacity();
     uint64_t len = 0;
     // repeated keys lower the line count: have the library count it exactly
-    // first (this builder's context belongs to its thread)
-    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 1);
+    // first (this builder's context belongs to its thread; the caller's
+    // setting is restored after the call)
+    uint64_t exact = 0;
+    if (dups_) {
+      dlsm_ctx_get_option(ctx_, DLSM_OPT_BUILD_EXACT, &exact);
+      dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 1);
+    }
     status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
-    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 0);
+    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
     clear_keys();
     result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
   void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
-  // Output goes to p from now on (full_filter_block.cc:146-148); cap is the
-  // size of p's buffer (the reference does not check; we do).
-  void Move_buffer(const char* p, size_t cap = SIZE_MAX) {
+  // Output goes to p from now on (full_filter_block.cc:144-146).  Every
+  // reference caller moves back into its own slot (local_filter_mr[0]->addr:
+  // table_builder_computeside.cc:566, table_builder_bacs.cpp:553,
+  // table_builder_bams.cpp:456); a buffer outside the slot must come with its
+  // size, or Finish refuses it (DLSM_E_CAPACITY) -- the reference's only
+  // check is an assert against the slot's length (full_filter_block.cc:103).
+  void Move_buffer(const char* p) { Move_buffer(p, 0); }
+  void Move_buffer(const char* p, size_t cap) {
     result.Reset(p, 0);
     moved_cap_ = cap;
+  }
+  // Bytes Finish may write at result.data(): the rest of the slot when the
+  // output lies inside it, else the size given to Move_buffer (0 if none).
+  size_t output_capacity() const {
+    const char* a = static_cast<const char*>(local_mr_->addr);
+    const char* p = result.data();
+    if (p >= a && p < a + local_mr_->length) return local_mr_->length - static_cast<size_t>(p - a);
+    return moved_cap_;
   }
   int num_probes() const { return num_probes_; }
   int status() const { return status_; }
@@ -217,7 +261,7 @@ class FullFilterBlockBuilder {
   bool uniform_ = true;
   size_t key_len_ = 0, last_len_ = 0;
   uint64_t n_ = 0, dups_ = 0;
-  size_t moved_cap_ = SIZE_MAX;
+  size_t moved_cap_ = 0;
   int status_ = DLSM_OK;
 
  public:

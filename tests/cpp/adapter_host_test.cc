@@ -1,0 +1,37 @@
+// Host-only checks of the C++ adapter (no GPU, no context): where Finish may
+// write after Move_buffer (full_filter_block.cc:144-146), and the staging
+// buffer's claim rules.  Built and run by tests/test_gpu_adapter.py on CPU.
+#include <cstdio>
+#include <vector>
+
+#include "dlsm_bloom_adapter.hpp"
+
+#define CHECK(c)                                              \
+  do {                                                        \
+    if (!(c)) {                                               \
+      std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+      return 1;                                               \
+    }                                                         \
+  } while (0)
+
+int main() {
+  std::vector<char> slot(256 * 1024), other(4096);
+  dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+  dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, nullptr);
+  CHECK(b.output_capacity() == slot.size());  // a fresh builder writes at the slot's start
+  b.Move_buffer(slot.data() + 1000);           // inside the slot: the rest of it
+  CHECK(b.output_capacity() == slot.size() - 1000);
+  b.Move_buffer(slot.data());                  // what every reference caller does
+  CHECK(b.output_capacity() == slot.size());
+  b.Move_buffer(other.data());                 // outside, size unknown: nothing may be written
+  CHECK(b.output_capacity() == 0);
+  b.Move_buffer(other.data(), other.size());   // outside with its size
+  CHECK(b.output_capacity() == other.size());
+  b.Reset();                                   // back to the slot (full_filter_block.cc:141-143)
+  CHECK(b.output_capacity() == slot.size());
+  // the staging-buffer claim needs a context
+  CHECK(dlsm_ctx_host_buffer_claim(nullptr, &b) == DLSM_E_ARG);
+  CHECK(dlsm_ctx_host_buffer_release(nullptr, &b) == DLSM_E_ARG);
+  std::printf("OK adapter host\n");
+  return 0;
+}

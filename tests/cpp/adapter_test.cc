@@ -255,6 +255,70 @@ int main() {
             (orc_filter_block_key_may_match(want.data(), wl, key_block[i],
                                             reinterpret_cast<const uint8_t*>(ks[i].data()), 20, 0) != 0));
   }
+  // ---- two live builders on ONE context: the second stages into a
+  // private pinned buffer, both filters stay exact ----
+  {
+    const int n1 = 40000, n2 = 70000;  // the second grows past the first's size
+    std::vector<char> s1(256 * 1024, 0), s2(256 * 1024, 0);
+    dlsm_adapter::FilterSlot m1{s1.data(), s1.size()}, m2{s2.data(), s2.size()};
+    dlsm_adapter::FullFilterBlockBuilder b1(&m1, 10, ctx), b2(&m2, 10, ctx);
+    std::string f1, f2;
+    std::vector<uint64_t> o1{0}, o2{0};
+    for (int i = 0; i < n2; i++) {  // interleaved, as two tables' iterators would be
+      uint8_t k[20];
+      if (i < n1) {
+        orc_dbbench_key(static_cast<uint64_t>(i) * 2, 20, k);
+        b1.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+        f1.append(reinterpret_cast<char*>(k), 20);
+        o1.push_back(f1.size());
+      }
+      orc_dbbench_key(static_cast<uint64_t>(i) * 2 + 1, 20, k);
+      b2.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+      f2.append(reinterpret_cast<char*>(k), 20);
+      o2.push_back(f2.size());
+    }
+    b1.Finish();
+    b2.Finish();
+    CHECK(b1.status() == DLSM_OK && b2.status() == DLSM_OK);
+    std::vector<uint8_t> w1(256 * 1024, 0), w2(256 * 1024, 0);
+    const int64_t l1 = orc_full_build(reinterpret_cast<const uint8_t*>(f1.data()), o1.data(), 0, n1, 10, w1.data(),
+                                      w1.size());
+    const int64_t l2 = orc_full_build(reinterpret_cast<const uint8_t*>(f2.data()), o2.data(), 0, n2, 10, w2.data(),
+                                      w2.size());
+    CHECK(static_cast<int64_t>(b1.result.size()) == l1 && std::memcmp(b1.result.data(), w1.data(), l1) == 0);
+    CHECK(static_cast<int64_t>(b2.result.size()) == l2 && std::memcmp(b2.result.data(), w2.data(), l2) == 0);
+  }
+  // ---- Move_buffer outside the slot: refused unless its size is given and
+  // holds the filter; the caller's BUILD_EXACT setting survives a Finish
+  // over repeated keys ----
+  {
+    std::vector<char> slot(256 * 1024, 0), other(4096, 0);
+    dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx);
+    CHECK(dlsm_ctx_set_option(ctx, DLSM_OPT_BUILD_EXACT, 2) == DLSM_OK);
+    auto add = [&](int n) {
+      for (int i = 0; i < n; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i / 2), 20, k);  // every key twice
+        b.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+      }
+    };
+    b.Move_buffer(other.data());  // no size: refused
+    add(10000);
+    b.Finish();
+    CHECK(b.status() == DLSM_E_CAPACITY && b.result.size() == 0);
+    b.Move_buffer(other.data(), other.size());  // 4 KiB < the 5,000-key filter's 6,341 bytes
+    add(10000);
+    b.Finish();
+    CHECK(b.status() == DLSM_E_CAPACITY && b.result.size() == 0);
+    b.Move_buffer(other.data(), other.size());
+    add(2000);  // 1,000 distinct keys: 1,349 bytes
+    b.Finish();
+    CHECK(b.status() == DLSM_OK && b.result.size() == 1349 && b.result.data() == other.data());
+    uint64_t ex = 99;
+    CHECK(dlsm_ctx_get_option(ctx, DLSM_OPT_BUILD_EXACT, &ex) == DLSM_OK && ex == 2);
+    CHECK(dlsm_ctx_set_option(ctx, DLSM_OPT_BUILD_EXACT, 0) == DLSM_OK);
+  }
   dlsm_ctx_destroy(ctx);
   std::printf("OK adapter\n");
   return 0;

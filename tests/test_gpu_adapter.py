@@ -63,6 +63,16 @@ def test_adapter_derives_from_host_filter_policy(tmp_path):
     assert subprocess.run([str(exe)], timeout=60).returncode == 0
 
 
+def test_adapter_output_capacity_on_cpu(tmp_path):
+    """Move_buffer: Finish writes at most the rest of the slot, or the size a
+    buffer outside the slot came with -- 0 (refused, DLSM_E_CAPACITY) when it
+    came without one (table/full_filter_block.cc:103,144-146).
+    Host logic only: runs without a GPU."""
+    exe = _compile(tmp_path, "adapter_host_test")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0 and "OK adapter host" in out.stdout, out.stdout + out.stderr
+
+
 @pytest.mark.gpu
 def test_adapter_on_gpu(tmp_path):
     exe = _compile(tmp_path, "adapter_test")
