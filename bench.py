@@ -8,16 +8,24 @@ One step = one pass of the path over one batch:
   * probe: 100 M 20-byte lookups (v = mt19937_64(1000) mod 25.6 M) against 8
     stacked per-level full filters (dlsm_bloom_full_probe_dev) -- configs[2].
 
---gpus N > 1 (one process per GPU, torch.distributed.run) defaults to STRONG
-scaling, the north star's config 4: the SAME 16 SSTables split s mod N, the
-filter set built once and broadcast to every rank, the ONE 100 M-key lookup
-stream split into N contiguous shards (dlsm_amd/sharding.py).  --scaling weak
-gives every rank its own 16 tables and 100 M lookups instead.
-value = (build keys + probe keys) of the whole job / max-over-ranks wall time.
-A rank whose build batch is under 16 M keys (strong scaling at N >= 2) runs
-its build and probe on two streams (--overlap auto|on|off).
+--gpus N > 1 is STRONG scaling, the north star's config 4: the SAME 16
+SSTables split s mod N, the filter set replicated on every GPU, the ONE 100
+M-key lookup stream split into N contiguous shards (dlsm_amd/sharding.py).
+Two launch shapes, same work:
+  * `python bench.py --gpus N`: ONE process, one host thread + dlsm_ctx +
+    stream per GPU (dLSM's builders are threads of one
+    process, db/db_impl.cc:3373-3386), dlsm_amd/multigpu.py.  Refuses to run
+    when fewer than N GPUs are visible; --rehearse maps the N logical devices
+    onto GPU 0 (a 1-GPU box runs the N-device code).
+  * `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`:
+    one process per GPU (RCCL only for the barrier, the max-over-ranks time and
+    the one-time filter broadcast); --gpus must equal WORLD_SIZE.
+--scaling weak (process mode) gives every rank its own 16 tables and 100 M
+lookups instead.  value = (build keys + probe keys) of the whole job / wall
+time of the slowest GPU.  A GPU whose build batch is under 16 M keys (strong
+scaling at N >= 2) runs its build and probe on two streams (--overlap).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--rehearse]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -91,9 +99,24 @@ def main():
                          "many CUs per XCD (1..4), every partition pass on the other CUs (0 = off)")
     ap.add_argument("--graph", type=int, default=0,
                     help="1: capture one step (build + probe launches) in a HIP graph and replay it")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="--gpus N in one process on a box with fewer GPUs: N logical devices on GPU 0")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
+
+    # launch shape: torchrun (WORLD_SIZE set) = one process per GPU, and its
+    # rank count must be the --gpus asked for; otherwise --gpus N > 1 = one
+    # process with a host thread per GPU
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
+            f"(--nproc-per-node {args.gpus}) or drop the launcher")
+        sys.exit(2)
+    if env_world is None and args.gpus > 1:
+        sys.exit(run_threads(args))
+    if args.rehearse and args.gpus == 1 and env_world is None:
+        log("bench.py: --rehearse only applies to --gpus N > 1")
 
     import numpy as np
     import torch
@@ -316,7 +339,13 @@ def main():
         result["roofline"]["traffic_source"] = traffic["source"]
         result["roofline"]["traffic_alg_ratio"] = round(
             traffic["traffic_bytes"] / (probe_bytes if dominant == "probe" else build_bytes), 3)
-    result["roofline"]["hbm_copy_GBs_measured"] = round(copy_bandwidth(dev, stream), 1)
+    ceil, shapes = stream_ceilings(dev, stream)
+    result["roofline"]["hbm_read_GBs_measured"] = ceil["read"]
+    result["roofline"]["hbm_copy_GBs_measured"] = ceil["copy"]
+    result["roofline"]["frac_of_measured_read"] = round(ach / ceil["read"], 4)
+    result["roofline"]["frac_of_measured_copy"] = round(ach / ceil["copy"], 4)
+    result["roofline"]["ceiling_kernels"] = ("dlsm_stream_kernel, best of plain/nt x grid-stride/chunked x "
+                                             f"1-4K workgroups of 512: {shapes}")
 
     # ---- host-inclusive (PCIe) rate, N=1 only: recorded, never `value` ----
     if world == 1 and not args.no_e2e:
@@ -341,6 +370,103 @@ def main():
         dist.destroy_process_group()
 
 
+def run_threads(args) -> int:
+    """--gpus N > 1 in one process: a host thread + dlsm_ctx + stream per GPU
+    (dlsm_amd/multigpu.py), strong scaling of config 4.  Returns the exit code."""
+    import numpy as np
+    import torch
+
+    from dlsm_amd import multigpu as MG
+
+    N_GPU = args.gpus
+    available = torch.cuda.device_count()  # counting does not initialise the GPU
+    try:
+        devices = MG.device_map(N_GPU, args.rehearse, available)
+    except MG.DeviceCountError as e:
+        log(f"bench.py: {e}")
+        return 2
+    if args.scaling == "weak":
+        log("bench.py: --scaling weak needs the process launcher (torchrun); one process runs strong scaling")
+        return 2
+    if args.cosched or args.graph or args.probe_round is not None or args.build_groups:
+        log("bench.py: --cosched / --graph / --probe-round / --build-groups are single-GPU A/B knobs")
+        return 2
+    N, T, Q, F, bpk = args.keys_per_table, args.tables, args.lookups, args.filters, args.bits_per_key
+    from dlsm_amd import workload as W
+
+    t_in = time.time()
+    stream_vals = W.mt19937_64(1000, Q) % np.uint64(2 * F * N)  # the ONE lookup stream, generated once
+    opts = MG.WorkerOptions(path=args.path, probe_chunk_lg=args.probe_chunk_lg, probe_slice_lg=args.probe_slice_lg,
+                            overlap=args.overlap, overlap_below=OVERLAP_BELOW, pass_events=True)
+    workers = MG.build_workers(N_GPU, devices, T, N, Q, F, bpk, opts, lookup_stream=stream_vals)
+    digests = {w.filter_digest() for w in workers}
+    if len(digests) != 1:
+        log("bench.py: the devices' filter sets differ")
+        return 3
+    for w in workers:
+        log(f"[gpu {w.rank} -> device {w.device}] tables {w.work.tables}, lookups "
+            f"[{w.work.lookup_lo}, {w.work.lookup_hi}), overlap {w.overlap}")
+    log(f"inputs ready in {time.time() - t_in:.1f}s")
+    elapsed = MG.timed_run(workers, args.steps, args.warmup)
+    w0 = workers[0]
+    w0.collect_pass_times()
+    build_ms = float(np.mean(w0.build_ms)) if w0.build_ms else float("nan")
+    probe_ms = float(np.mean(w0.probe_ms)) if w0.probe_ms else float("nan")
+    value = (T * N + Q) * args.steps / elapsed / 1e6
+    inp = w0.inp
+    filt_bytes = sum(int(f.numel()) for f in inp.filters)
+    nb = max(1, len(inp.tables) * N)
+    probe_bytes = inp.lookups.n * (20 + inp.fs.mask_bytes) + filt_bytes
+    build_bytes = len(inp.tables) * N * 20 + int(inp.lens.cpu().numpy()[: len(inp.tables)].sum())
+    probe_gbs = probe_bytes / (probe_ms * 1e-3) / 1e9
+    build_gbs = build_bytes / (build_ms * 1e-3) / 1e9
+    dominant = "probe" if probe_ms >= build_ms else "build"
+    ach = probe_gbs if dominant == "probe" else build_gbs
+    result = {
+        "metric": "Bloom build+probe Mkeys/s (device-resident), 20B keys, 10 bits/key",
+        "value": round(value, 2),
+        "unit": "Mkeys/s",
+        "n_gpus": N_GPU,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic db_bench keys (GenerateKeyFromInt), mt19937_64 lookups",
+        "config": {
+            "workload": (f"build {T} SSTable full filters x {N} keys + probe {Q} lookups vs {F} stacked "
+                         f"filters, split over {N_GPU} GPUs"),
+            "key_bytes": 20, "bits_per_key": bpk, "tables": T, "keys_per_table": N,
+            "lookups": Q, "filters": F,
+            "parallelism": (f"strong: {T} SSTables split s mod {N_GPU}, filters replicated, {Q} lookups "
+                            f"sharded x{N_GPU}; one process, one host thread + context + stream per GPU"),
+            "launch": "threads",
+            "devices": devices,
+            "rehearsal": bool(args.rehearse),
+            "gpu_tables": [w.work.tables for w in workers],
+            "gpu_lookups": [[w.work.lookup_lo, w.work.lookup_hi] for w in workers],
+            "overlap": [w.overlap for w in workers],
+            "path": {0: "auto", 1: "direct", 2: "sliced"}[args.path],
+            "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": f"{dominant} pass (GPU 0's share)", "achieved": round(ach, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "traffic": None,
+        },
+        "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
+                  "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
+        "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, inp.lookups.n) / probe_ms / 1e3, 1),
+                  "alg_GBs": round(probe_gbs, 1), "alg_bytes_per_key": round(probe_bytes / max(1, inp.lookups.n), 3)},
+    }
+    print(json.dumps(result), flush=True)
+    for w in workers:
+        w.close()
+    return 0
+
+
 def load_traffic(path, config, dominant):
     """Per-launch fabric bytes of the dominant pass from a committed PMC
     summary (scripts/pmc_traffic.py), only if it was collected on this config."""
@@ -354,24 +480,42 @@ def load_traffic(path, config, dominant):
     return {"traffic_bytes": d["traffic_bytes"], "source": t["source"]} if d else None
 
 
-def copy_bandwidth(dev, stream, nbytes=1 << 30, reps=10):
-    """Measured device-to-device streaming rate (read + write bytes / s, GB/s)
-    on this box: the achievable HBM ceiling beside the 8 TB/s spec peak."""
+def stream_ceilings(dev, stream, nbytes=1 << 31, reps=5):
+    """The box's own HBM streaming ceilings, measured in this run with the
+    library's 16-byte-per-lane kernels (dlsm_stream_kernel): the best of the
+    read-only and of the copy shapes (plain / non-temporal, grid-stride /
+    one range per workgroup, 1-4 K workgroups).  GB/s of bytes moved (copy:
+    read + write)."""
+    import ctypes
+
     import torch
 
-    with torch.cuda.stream(stream):
-        a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        b = torch.empty_like(a)
-        b.copy_(a)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            b.copy_(a)
-        e1.record(stream)
-    stream.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    del a, b
-    return 2 * nbytes / (ms * 1e-3) / 1e9
+    import dlsm_amd
+
+    fn = dlsm_amd.lib().dlsm_stream_kernel
+    src = torch.zeros(nbytes, dtype=torch.uint8, device=dev)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    raw = ctypes.c_void_p(stream.cuda_stream)
+    best = {}
+    for kind, name in ((0, "read"), (1, "copy")):
+        for variant in range(4):
+            for blocks in (1024, 2048, 4096):
+                args = (raw, kind, variant, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()),
+                        ctypes.c_uint64(nbytes), ctypes.c_uint32(blocks))
+                if fn(*args) != 0:
+                    raise RuntimeError("dlsm_stream_kernel failed")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(reps):
+                    fn(*args)
+                e1.record(stream)
+                stream.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                gbs = nbytes * (1 + kind) / (ms * 1e-3) / 1e9
+                if gbs > best.get(name, (0,))[0]:
+                    best[name] = (gbs, {"variant": variant, "blocks": blocks, "ms": round(ms, 4)})
+    del src, dst
+    return {k: round(v[0], 1) for k, v in best.items()}, {k: v[1] for k, v in best.items()}
 
 
 def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):

@@ -343,6 +343,23 @@ class Context:
         check(lib().dlsm_bloom_full_build_dev(self.h, jobs, len(tables), bits_per_key,
                                               _ptr(out_lens)), "full_build_dev")
 
+    def bind_full_build_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
+        """full_build_dev with its arguments marshalled once: returns a
+        zero-argument callable (one ctypes call per invocation; the GIL is
+        released inside it), for per-step loops on several host threads."""
+        caps = [int(o.numel()) for o in outs]
+        jobs = self._jobs(tables, outs, caps)
+        fn, h, n, lp = lib().dlsm_bloom_full_build_dev, self.h, len(tables), _ptr(out_lens)
+        keep = (jobs, list(tables), list(outs), out_lens)
+
+        def call():
+            st = fn(h, jobs, n, bits_per_key, lp)
+            if st:
+                check(st, "full_build_dev")
+
+        call.keep = keep
+        return call
+
     def full_build_block(self, tables: Sequence[Keys], bits_per_key: int = 10, caps=None) -> list:
         """Filter + 5-byte block trailer (FinishFilterBlock), host in/out."""
         n = len(tables)
@@ -444,6 +461,20 @@ class Context:
         ks = keys.c()
         check(lib().dlsm_bloom_full_probe_dev(self.h, fs.h, C.byref(ks), _ptr(mask)),
               "full_probe_dev")
+
+    def bind_full_probe_dev(self, fs: FilterSet, keys: Keys, mask):
+        """full_probe_dev with its arguments marshalled once (see bind_full_build_dev)."""
+        ks = keys.c()
+        fn, h, fh, kp, mp = lib().dlsm_bloom_full_probe_dev, self.h, fs.h, C.byref(ks), _ptr(mask)
+        keep = (ks, fs, keys, mask)
+
+        def call():
+            st = fn(h, fh, kp, mp)
+            if st:
+                check(st, "full_probe_dev")
+
+        call.keep = keep
+        return call
 
     # -- legacy FilterPolicy format -----------------------------------------
     def legacy_build(self, tables: Sequence[Keys], bits_per_key: int = 10) -> list:

@@ -115,6 +115,7 @@ SIGNATURES = [
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_legacy_probe", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_stream_kernel", C.c_int, [_VP, C.c_int, C.c_int, _VP, _VP, C.c_uint64, C.c_uint32]),
 ]
 
 _LIB = None

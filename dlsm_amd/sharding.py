@@ -115,11 +115,14 @@ class RankInputs:
 
 
 def make_inputs(ctx, work: RankWork, keys_per_table: int, n_filters: int, bits_per_key: int,
-                dev, stream=None, dist=None) -> RankInputs:
+                dev, stream=None, dist=None, lookup_shard=None) -> RankInputs:
     """Materialise a rank's inputs in HBM (untimed set-up).  The filter set is
     built once -- by rank 0 in strong scaling, then broadcast to every rank
     (the one-time exchange of SURVEY.md §8e; RCCL over xGMI with the nccl
-    backend, host memory with gloo) -- and every rank keeps its own copy."""
+    backend, host memory with gloo) -- and every rank keeps its own copy.
+    Without `dist` (one process, a thread per GPU) each device builds the set
+    from the same keys.  `lookup_shard`: this rank's shard of the lookup
+    stream when the caller generated the stream once (else generated here)."""
     import contextlib
 
     import numpy as np
@@ -168,7 +171,7 @@ def make_inputs(ctx, work: RankWork, keys_per_table: int, n_filters: int, bits_p
                 fouts[f].copy_(h.to(dev))
     torch.cuda.synchronize(dev)
     fs = ctx.filterset(fouts, on_device=True)
-    qv = lookup_values(work, 2 * F * N)
+    qv = lookup_shard if lookup_shard is not None else lookup_values(work, 2 * F * N)
     with ctxm:
         q = W.dbbench_keys_torch(torch.from_numpy(qv.astype(np.int64)).to(dev))
         mask = torch.empty(max(1, work.n_lookups) * fs.mask_bytes, dtype=torch.uint8, device=dev)

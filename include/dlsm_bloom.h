@@ -381,6 +381,17 @@ int dlsm_filter_block_build(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64
 int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, const dlsm_keyset* keys,
                             const uint64_t* block_offsets, uint8_t* out);
 
+/* ---- measurement helper (not on the filter path) ------------------------ */
+
+/* The box's HBM streaming ceilings for the roofline (bench.py): launch one
+ * 16-byte-per-lane streaming kernel on hip_stream over `bytes` (a multiple of
+ * 16; 16-byte-aligned buffers).  kind 0: read src (dst receives at most 512
+ * u32 of sink writes, normally none); kind 1: copy src -> dst.  variant bit
+ * 0: non-temporal accesses; bit 1: one contiguous range per workgroup (else
+ * grid-stride).  blocks: workgroups of 512 threads.  Asynchronous. */
+int dlsm_stream_kernel(void* hip_stream, int kind, int variant, const void* src, void* dst, uint64_t bytes,
+                       uint32_t blocks);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -1,0 +1,113 @@
+"""`bench.py --gpus N` in ONE process, a host thread + context + stream per GPU
+(dlsm_amd/multigpu.py; SURVEY.md §8d config 4, "all GPUs launched
+concurrently from one host thread per GPU").
+
+* CPU: the launch-shape rules -- N > visible GPUs exits non-zero instead of
+  silently running one GPU, --gpus must equal a launcher's WORLD_SIZE, the
+  rehearsal map, the device map of a full node.
+* GPU (-m gpu): two logical devices rehearsed on GPU 0 through the bench's own
+  worker code (build_workers / timed_run): the union of the two devices'
+  filters and the concatenation of their mask shards equal the oracle's
+  single-device answer, and `bench.py --gpus 2 --rehearse` prints
+  n_gpus 2 with tables [0,2,..]/[1,3,..] and lookups [0,Q/2)/[Q/2,Q).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    if env:
+        e.update(env)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True,
+                          text=True, timeout=timeout, env=e, cwd=ROOT)
+
+
+def test_device_map_rules():
+    from dlsm_amd import multigpu as MG
+
+    assert MG.device_map(8, False, 8) == list(range(8))
+    assert MG.device_map(4, False, 8) == [0, 1, 2, 3]
+    assert MG.device_map(2, True, 1) == [0, 0]
+    with pytest.raises(MG.DeviceCountError):
+        MG.device_map(8, False, 1)
+    with pytest.raises(MG.DeviceCountError):
+        MG.device_map(2, True, 0)
+
+
+def test_too_many_gpus_exits_nonzero():
+    """No silent one-GPU run: --gpus 8 where fewer GPUs are visible fails."""
+    import torch
+
+    if torch.cuda.device_count() >= 8:
+        pytest.skip("this node has 8 GPUs")
+    r = _bench(["--gpus", "8", "--steps", "1", "--warmup", "0", "--no-cpu", "--no-e2e"])
+    assert r.returncode != 0
+    assert "GPUs but only" in r.stderr, r.stderr[-2000:]
+
+
+def test_gpus_must_match_launcher_world_size():
+    r = _bench(["--gpus", "1", "--steps", "1", "--warmup", "0"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, r.stderr[-2000:]
+    r = _bench(["--gpus", "4", "--steps", "1", "--warmup", "0"], env={"WORLD_SIZE": "2", "RANK": "0"})
+    assert r.returncode == 2
+
+
+# ---------------------------------------------------------------------------
+# GPU: two logical devices on GPU 0
+# ---------------------------------------------------------------------------
+_T, _N, _Q, _F = 16, 20_000, 1_000_003, 8
+
+
+@pytest.mark.gpu
+def test_two_logical_devices_strong_scaling_parity(orc):
+    from dlsm_amd import multigpu as MG
+
+    opts = MG.WorkerOptions(overlap="auto", overlap_below=16_000_000, pass_events=True)
+    workers = MG.build_workers(2, [0, 0], _T, _N, _Q, _F, 10, opts,
+                               lookup_stream=orc.mt_values(1000, 2 * _F * _N, _Q))
+    try:
+        dt = MG.timed_run(workers, steps=3, warmup=1)
+        assert dt > 0
+        workers[0].collect_pass_times()
+        assert len(workers[0].probe_ms) == 3 and len(workers[1].probe_ms) == 0
+        assert [w.work.tables for w in workers] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
+        assert [(w.work.lookup_lo, w.work.lookup_hi) for w in workers] == [(0, _Q // 2), (_Q // 2, _Q)]
+        union = {}
+        for w in workers:
+            L = w.inp.lens.cpu().numpy()
+            for j, s in enumerate(w.work.tables):
+                union[s] = w.inp.outs[j][: int(L[j])].cpu().numpy().tobytes()
+        for s in range(_T):
+            assert union[s] == orc.full_build(orc.dbbench_keys(s, _T, _N), _N), s
+        filters = [orc.full_build(orc.dbbench_keys(f, _F, _N), _N) for f in range(_F)]
+        for w in workers:
+            assert [f.cpu().numpy().tobytes() for f in w.inp.filters] == filters
+        qk = orc.keys_from_values(orc.mt_values(1000, 2 * _F * _N, _Q))
+        want = orc.full_probe(filters, qk, _Q, nthreads=8)
+        got = np.concatenate([w.inp.mask[: w.work.n_lookups].cpu().numpy() for w in workers])
+        assert got.size == _Q and np.array_equal(got, want)
+    finally:
+        for w in workers:
+            w.close()
+
+
+@pytest.mark.gpu
+def test_bench_two_gpus_rehearsed():
+    r = _bench(["--gpus", "2", "--rehearse", "--steps", "3", "--warmup", "1", "--keys-per-table", "200000",
+                "--lookups", "4000000"], timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["config"]["launch"] == "threads"
+    assert line["config"]["devices"] == [0, 0] and line["config"]["rehearsal"]
+    assert line["config"]["gpu_tables"] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
+    assert line["config"]["gpu_lookups"] == [[0, 2_000_000], [2_000_000, 4_000_000]]
+    assert line["value"] > 0 and line["roofline"]["achieved"] > 0
