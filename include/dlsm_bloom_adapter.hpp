@@ -166,7 +166,7 @@ class FullFilterBlockBuilder {
   // LDS-tiled key loaders) and whether a key repeats its predecessor (then
   // the line count is counted exactly before bucketing: DLSM_OPT_BUILD_EXACT).
   void AddKey(const Slice& key) {
-    if (status_ != DLSM_OK) return;  // staging failed: Finish reports it
+    if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
     const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
     if (n_ == 0) {
       key_len_ = key.size();
@@ -179,7 +179,7 @@ class FullFilterBlockBuilder {
       }
     }
     if (!keys_.append(key.data(), key.size())) {
-      status_ = DLSM_E_NOMEM;
+      stage_status_ = DLSM_E_NOMEM;
       return;
     }
     if (!uniform_) offsets_.push_back(keys_.size());
@@ -189,7 +189,8 @@ class FullFilterBlockBuilder {
   // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
   // buffer (the slot, or the buffer given to Move_buffer).
   void Finish() {
-    if (status_ != DLSM_OK) {
+    if (stage_status_ != DLSM_OK) {
+      status_ = stage_status_;
       result.Reset(result.data(), 0);
       clear_keys();
       return;
@@ -251,6 +252,7 @@ class FullFilterBlockBuilder {
     uniform_ = true;
     key_len_ = last_len_ = 0;
     n_ = dups_ = 0;
+    stage_status_ = DLSM_OK;
   }
   FilterSlot* local_mr_;
   int bits_per_key_;
@@ -262,7 +264,8 @@ class FullFilterBlockBuilder {
   size_t key_len_ = 0, last_len_ = 0;
   uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = 0;
-  int status_ = DLSM_OK;
+  int status_ = DLSM_OK;        // the last Finish's result
+  int stage_status_ = DLSM_OK;  // key staging of the current table
 
  public:
   Slice result;  // Filter data computed so far

@@ -23,6 +23,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def run_check(num=6_250_000, threads=16, every=97, gets=2_000_000, progress=None):
+    """The replay at `num` writes per thread with oracle sampling; returns the
+    replay record with an "oracle_check" entry.  `progress`: a callable given a
+    line every ~20 s (a long run must show activity)."""
+    import dbbench_replay as R
+    import oracle
+
+    chk = {"filters_checked": 0, "filters_bad": 0, "gets_checked": 0, "gets_bad": 0, "builds_seen": 0}
+    t_last = [time.time()]
+    say = progress or (lambda m: print(m, file=sys.stderr, flush=True))
+
+    def on_build(values, filters):
+        for v, f in zip(values, filters):
+            chk["builds_seen"] += 1
+            if chk["builds_seen"] % every == 1:
+                chk["filters_checked"] += 1
+                if f != oracle.full_build(oracle.keys_from_values(v), v.size):
+                    chk["filters_bad"] += 1
+        if time.time() - t_last[0] > 20:  # progress for the hang detector
+            t_last[0] = time.time()
+            say(f"[replay] {chk['builds_seen']} filters built")
+
+    def on_read(b0, vals, masks, files):
+        if b0 == 0:
+            n = min(gets, vals.size)
+            fo = [type("F", (), dict(level=f.level, number=f.number, smallest=f.smallest, largest=f.largest,
+                                     largest_trailer=f.largest_trailer, filter=f.filter)) for f in files]
+            want, _ = oracle.version_probe(fo, oracle.keys_from_values(vals[:n]), n, (1 << 56) - 1)
+            chk["gets_checked"] = n
+            chk["gets_bad"] = int(np.count_nonzero(want != masks[:n]))
+        say(f"[replay] reads from {b0}")
+
+    res, _ = R.run(num, threads, 10, on_build=on_build, on_read=on_read)
+    res["oracle_check"] = chk
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--num", type=int, default=6_250_000)
@@ -30,35 +67,8 @@ def main():
     ap.add_argument("--every", type=int, default=97)
     ap.add_argument("--gets", type=int, default=2_000_000)
     args = ap.parse_args()
-
-    import dbbench_replay as R
-    import oracle
-
-    chk = {"filters_checked": 0, "filters_bad": 0, "gets_checked": 0, "gets_bad": 0, "builds_seen": 0}
-    t_last = [time.time()]
-
-    def on_build(values, filters):
-        for v, f in zip(values, filters):
-            chk["builds_seen"] += 1
-            if chk["builds_seen"] % args.every == 1:
-                chk["filters_checked"] += 1
-                if f != oracle.full_build(oracle.keys_from_values(v), v.size):
-                    chk["filters_bad"] += 1
-        if time.time() - t_last[0] > 30:  # progress for the hang detector
-            t_last[0] = time.time()
-            print(f"[replay] {chk['builds_seen']} filters built", file=sys.stderr, flush=True)
-
-    def on_read(b0, vals, masks, files):
-        if b0 == 0:
-            n = min(args.gets, vals.size)
-            fo = [type("F", (), dict(level=f.level, number=f.number, smallest=f.smallest, largest=f.largest,
-                                     largest_trailer=f.largest_trailer, filter=f.filter)) for f in files]
-            want, _ = oracle.version_probe(fo, oracle.keys_from_values(vals[:n]), n, (1 << 56) - 1)
-            chk["gets_checked"] = n
-            chk["gets_bad"] = int(np.count_nonzero(want != masks[:n]))
-
-    res, _ = R.run(args.num, args.threads, 10, on_build=on_build, on_read=on_read)
-    res["oracle_check"] = chk
+    res = run_check(args.num, args.threads, args.every, args.gets)
+    chk = res["oracle_check"]
     print(json.dumps(res), flush=True)
     if chk["filters_bad"] or chk["gets_bad"]:
         raise SystemExit(1)

@@ -71,3 +71,34 @@ def test_replay_parity_with_compactions(gpu):
         want, _ = oracle.version_probe(_files_for_oracle(files), oracle.keys_from_values(vals), vals.size,
                                        (1 << 56) - 1)
         assert np.array_equal(masks, want)
+
+
+@pytest.mark.gpu
+def test_replay_config5_full_size(gpu):
+    """BASELINE config 5 at its stated size: db_bench --num=6250000 x 16
+    threads = 100 M fillrandom writes (651 flushes + leveled compactions, every
+    filter built on the GPU from host keys into host slots, H2D/D2H included)
+    then 100 M readrandom Gets over the final version
+    (benchmarks/db_bench.cc:943-947,1232,1379-1404).  Oracle-sampled: every
+    97th filter byte for byte, and the first 2 M Gets' per-file answers.
+    Progress goes to gpurun_out/ every ~20 s (pytest holds stdout/stderr)."""
+    import json
+    import os
+    import time
+
+    import replay_fullsize_check as RC
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    prog = os.path.join(root, "gpurun_out", "replay_fullsize.progress")
+
+    def progress(msg):
+        with open(prog, "a") as f:
+            f.write(f"{time.time():.0f} {msg}\n")
+
+    res = RC.run_check(6_250_000, 16, 97, 2_000_000, progress=progress)
+    chk = res["oracle_check"]
+    progress("done " + json.dumps(chk))
+    assert res["fill"]["writes"] == 100_000_000
+    assert chk["filters_checked"] > 1000 and chk["filters_bad"] == 0
+    assert chk["gets_checked"] == 2_000_000 and chk["gets_bad"] == 0
