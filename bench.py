@@ -407,11 +407,12 @@ def run_threads(args) -> int:
         log(f"[gpu {w.rank} -> device {w.device}] tables {w.work.tables}, lookups "
             f"[{w.work.lookup_lo}, {w.work.lookup_hi}), overlap {w.overlap}")
     log(f"inputs ready in {time.time() - t_in:.1f}s")
-    elapsed = MG.timed_run(workers, args.steps, args.warmup)
+    # the timed steps run from the library's native runner: a std::thread per
+    # device, host barriers around the timed region (dlsm_multi_device_run)
+    elapsed, passes = MG.native_timed_run(workers, args.steps, args.warmup, bpk)
     w0 = workers[0]
-    w0.collect_pass_times()
-    build_ms = float(np.mean(w0.build_ms)) if w0.build_ms else float("nan")
-    probe_ms = float(np.mean(w0.probe_ms)) if w0.probe_ms else float("nan")
+    build_ms = float(np.mean([b for b, _ in passes]))
+    probe_ms = float(np.mean([p for _, p in passes]))
     value = (T * N + Q) * args.steps / elapsed / 1e6
     inp = w0.inp
     filt_bytes = sum(int(f.numel()) for f in inp.filters)
@@ -442,7 +443,7 @@ def run_threads(args) -> int:
             "lookups": Q, "filters": F,
             "parallelism": (f"strong: {T} SSTables split s mod {N_GPU}, filters replicated, {Q} lookups "
                             f"sharded x{N_GPU}; one process, one host thread + context + stream per GPU"),
-            "launch": "threads",
+            "launch": "threads (dlsm_multi_device_run)",
             "devices": devices,
             "rehearsal": bool(args.rehearse),
             "gpu_tables": [w.work.tables for w in workers],

@@ -35,6 +35,12 @@ class dlsm_build_job(C.Structure):
     _fields_ = [("keys", dlsm_keyset), ("out", C.c_void_p), ("out_cap", C.c_uint64)]
 
 
+class dlsm_device_work(C.Structure):
+    _fields_ = [("probe_ctx", C.c_void_p), ("build_ctx", C.c_void_p), ("jobs", C.c_void_p),
+                ("n_jobs", C.c_int), ("out_len_dev", C.c_void_p), ("fs", C.c_void_p),
+                ("keys", dlsm_keyset), ("mask_dev", C.c_void_p)]
+
+
 class dlsm_version_file(C.Structure):
     _fields_ = [("smallest_user_key", C.c_void_p), ("smallest_len", C.c_uint64),
                 ("largest_user_key", C.c_void_p), ("largest_len", C.c_uint64),
@@ -116,6 +122,9 @@ SIGNATURES = [
     ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_legacy_probe", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_stream_kernel", C.c_int, [_VP, C.c_int, C.c_int, _VP, _VP, C.c_uint64, C.c_uint32]),
+    ("dlsm_ctx_device", C.c_int, [_VP]),
+    ("dlsm_multi_device_run", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
+                                       C.POINTER(C.c_double), C.POINTER(C.c_float)]),
 ]
 
 _LIB = None

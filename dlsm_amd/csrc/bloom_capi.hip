@@ -448,6 +448,8 @@ int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* s) {
 
 void* dlsm_ctx_stream(dlsm_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
 
+int dlsm_ctx_device(const dlsm_ctx* ctx) { return ctx ? ctx->device : -1; }
+
 int dlsm_ctx_set_partition_stream(dlsm_ctx* ctx, void* s, uint32_t cus) {
   if (!ctx) return DLSM_E_ARG;
   ctx->pstream = static_cast<hipStream_t>(s);

@@ -140,6 +140,27 @@ class DeviceWorker:
             self.build_ms = [e[0].elapsed_time(e[1]) for e in evs]
             self.probe_ms = [e[2].elapsed_time(e[3]) for e in evs]
 
+    def device_work(self):
+        """This device's dlsm_device_work (the native runner's argument)."""
+        import ctypes as C
+
+        from . import _lib as L
+        from . import _ptr
+
+        inp = self.inp
+        caps = [int(o.numel()) for o in inp.outs]
+        jobs = self.ctx_b._jobs(inp.tables, inp.outs, caps)
+        w = L.dlsm_device_work()
+        w.probe_ctx, w.build_ctx = self.ctx.h.value, self.ctx_b.h.value
+        w.jobs = C.cast(jobs, C.c_void_p).value
+        w.n_jobs = len(inp.tables)
+        w.out_len_dev = _ptr(inp.lens)
+        w.fs = inp.fs.h.value if inp.lookups.n else None
+        w.keys = inp.lookups.c()
+        w.mask_dev = _ptr(inp.mask)
+        self._work_keep = (jobs, w)
+        return w
+
     def filter_digest(self) -> int:
         """Checksum of this device's stacked-filter inputs (all devices must agree)."""
         import hashlib
@@ -230,6 +251,24 @@ def timed_run(workers, steps: int, warmup: int):
     if t0 is None or t1 is None:
         raise RuntimeError("a device worker failed before the timed region ended")
     return t1 - t0
+
+
+def native_timed_run(workers, steps: int, warmup: int, bits_per_key: int):
+    """The timed region run by the library's native runner
+    (dlsm_multi_device_run: a std::thread per device, host barriers on both
+    sides of the timed steps, device 0's passes timed with HIP events).
+    Returns (seconds, [(build_ms, probe_ms) per step] of device 0)."""
+    import ctypes as C
+
+    from . import _lib as L
+    from . import check, lib
+
+    arr = (L.dlsm_device_work * len(workers))(*[w.device_work() for w in workers])
+    wall = C.c_double(0.0)
+    pm = (C.c_float * (2 * steps))()
+    check(lib().dlsm_multi_device_run(arr, len(workers), bits_per_key, steps, warmup, C.byref(wall), pm),
+          "multi_device_run")
+    return wall.value, [(pm[2 * i], pm[2 * i + 1]) for i in range(steps)]
 
 
 def build_workers(n_gpus: int, devices: list, T: int, N: int, Q: int, F: int, bpk: int,

@@ -117,6 +117,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx);
  * restores the context's own stream. */
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
 void* dlsm_ctx_stream(dlsm_ctx* ctx);
+/* The device a context runs on (-1 for NULL). */
+int dlsm_ctx_device(const dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
 /* Run the HBM-bound partition passes of sliced builds (one job group) and of
  * single-group probes (one round) on `hip_stream`, and the LDS-bound slice and
@@ -380,6 +382,34 @@ int dlsm_filter_block_build(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64
                             uint8_t* out, uint64_t out_cap, uint64_t* out_len);
 int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, const dlsm_keyset* keys,
                             const uint64_t* block_offsets, uint8_t* out);
+
+/* ---- several GPUs from one process -------------------------------------- */
+
+/* One device's share of a flush/compaction round plus a Get batch: its
+ * SSTables' build jobs (device pointers) and its shard of the lookups against
+ * its own copy of the stacked filter set (SSTables are
+ * independent, so nothing crosses devices). */
+typedef struct {
+  dlsm_ctx* probe_ctx;         /* the device's probe context (its stream) */
+  dlsm_ctx* build_ctx;         /* == probe_ctx, or a second context on the same device: the
+                                  build then runs on its stream beside the probe */
+  const dlsm_build_job* jobs;  /* n_jobs SSTables (device keys, device slots) */
+  int n_jobs;
+  uint64_t* out_len_dev;       /* device uint64[n_jobs] */
+  const dlsm_filterset* fs;    /* NULL: no probe */
+  dlsm_keyset keys;            /* device lookup shard */
+  uint8_t* mask_dev;
+} dlsm_device_work;
+
+/* Run `warmup` untimed then `steps` timed steps (build, then probe) on every
+ * entry concurrently, one host thread per entry (dLSM's shape: its builders
+ * are threads of one process, db/db_impl.cc:3373-3386).  The timed region
+ * starts when every device is idle and ends when every device has drained
+ * (host barriers on both sides): wall_seconds is the slowest device's.
+ * pass_ms (host float[2 * steps], or NULL): entry 0's build / probe time per
+ * step from HIP events on the streams they run on. */
+int dlsm_multi_device_run(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps, int warmup,
+                          double* wall_seconds, float* pass_ms);
 
 /* ---- measurement helper (not on the filter path) ------------------------ */
 
