@@ -121,8 +121,15 @@ SIGNATURES = [
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_legacy_probe", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_full_build_hashed_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
+    ("dlsm_bloom_full_build_hashed", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_stream_kernel", C.c_int, [_VP, C.c_int, C.c_int, _VP, _VP, C.c_uint64, C.c_uint32]),
     ("dlsm_ctx_device", C.c_int, [_VP]),
+    ("dlsm_batcher_create", C.c_int, [C.c_int, C.c_int, C.c_uint32, C.c_uint32, C.POINTER(_VP)]),
+    ("dlsm_batcher_destroy", C.c_int, [_VP]),
+    ("dlsm_batcher_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, _U64P]),
+    ("dlsm_batcher_full_build_hashed", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, _U64P]),
+    ("dlsm_batcher_stats", C.c_int, [_VP, _U64P, _U64P, _U64P]),
     ("dlsm_multi_device_run", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(C.c_double), C.POINTER(C.c_float)]),
 ]

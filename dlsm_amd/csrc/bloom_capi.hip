@@ -636,8 +636,16 @@ int dlsm_host_free(void* p) {
 // ---------------------------------------------------------------------------
 // Full filter build
 // ---------------------------------------------------------------------------
-int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
-                              int bits_per_key, uint64_t* out_len_dev) {
+namespace {
+
+// Hashed jobs: keys.bytes holds n BloomHash values (u32, 4-byte aligned,
+// key_len 4, no offsets) -- what AddKey computed on the host.
+bool is_hash_set(const dlsm_keyset& k) {
+  return k.offsets == nullptr && k.key_len == 4 && k.suffix_len == 0 && (k.n == 0 || aligned(k.bytes, 4));
+}
+
+int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                        uint64_t* out_len_dev, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
@@ -647,6 +655,7 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   for (int j = 0; j < n_jobs; j++) {
     const dlsm_build_job& b = jobs[j];
     DLSM_CHECK(validate_keyset(b.keys));
+    if (hashed && !is_hash_set(b.keys)) return DLSM_E_ARG;
     if (!b.out || !aligned(b.out, 16)) return DLSM_E_ARG;
     if (b.keys.n > 0xffffffffull * kBuildChunk) return DLSM_E_ARG;
     Ls[j] = full_num_lines(b.keys.n, bits_per_key, nullptr);
@@ -656,7 +665,7 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   int lgR = choose_build_lgR(Ls);
   if (lgR < 0) sliced_ok = false;
   if (ctx->path == 2 && !sliced_ok) return DLSM_E_ARG;
-  const int mode = all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC);
+  const int mode = hashed ? KM_HASH : (all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC));
   // Exact line counts (a count pass before the partition) where duplicate
   // user keys are expected to lower L below the speculative n-key count:
   // internal keys (several versions of a user key, suffix_len 8) and the
@@ -666,7 +675,9 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   // fallback for the rare batch whose duplicates do change L.
   bool any_suffix = false;
   for (int j = 0; j < n_jobs; j++) any_suffix = any_suffix || jobs[j].keys.suffix_len > 0;
-  const bool exact = sliced_ok && (ctx->build_exact == 1 ||
+  // Hashed jobs always count first: the entries keep no key to re-hash, so
+  // the slice pass's fallback for a lowered line count is not available.
+  const bool exact = sliced_ok && (hashed || ctx->build_exact == 1 ||
                                    (ctx->build_exact == 0 && (any_suffix || mode == KM_GENERIC)));
 
   std::vector<FullJobDev> hj(n_jobs);
@@ -761,6 +772,18 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
   return DLSM_OK;
 }
 
+}  // namespace
+
+int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                              int bits_per_key, uint64_t* out_len_dev) {
+  return full_build_dev_impl(ctx, jobs, n_jobs, bits_per_key, out_len_dev, false);
+}
+
+int dlsm_bloom_full_build_hashed_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                     int bits_per_key, uint64_t* out_len_dev) {
+  return full_build_dev_impl(ctx, jobs, n_jobs, bits_per_key, out_len_dev, true);
+}
+
 namespace {
 
 // Stage host keysets into one device buffer; returns per-job device keysets.
@@ -804,8 +827,9 @@ int stage_keys(dlsm_ctx* ctx, const dlsm_keyset* const* sets, int n, std::vector
 
 }  // namespace
 
-int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
-                          uint64_t* out_len) {
+namespace {
+int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                         uint64_t* out_len, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
@@ -831,7 +855,7 @@ int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
   DLSM_CHECK(ctx->st_out.ensure(obytes + 256));
   DLSM_CHECK(ctx->st_len.ensure(n_jobs));
   for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
-  DLSM_CHECK(dlsm_bloom_full_build_dev(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p));
+  DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p, hashed));
   hipStream_t s = ctx->stream;
   DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
   DLSM_TRY(hipStreamSynchronize(s));
@@ -845,6 +869,17 @@ int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
   }
   DLSM_TRY(hipStreamSynchronize(s));
   return st;
+}
+}  // namespace
+
+int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                          uint64_t* out_len) {
+  return full_build_host_impl(ctx, jobs, n_jobs, bits_per_key, out_len, false);
+}
+
+int dlsm_bloom_full_build_hashed(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
+                                 uint64_t* out_len) {
+  return full_build_host_impl(ctx, jobs, n_jobs, bits_per_key, out_len, true);
 }
 
 // ---------------------------------------------------------------------------

@@ -1664,6 +1664,9 @@ hipError_t launch_full_count(const FullJobDev* jobs, const uint32_t* chunk0s, in
   if (mode == KM_K20)
     full_partition_kernel<KM_K20, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                           nullptr, nullptr, 0, 0u);
+  else if (mode == KM_HASH)
+    full_partition_kernel<KM_HASH, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
+                                                                           nullptr, nullptr, 0, 0u);
   else if (mode == KM_K28)
     full_partition_kernel<KM_K28, false><<<total_chunks, kPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, dchunk,
                                                                           nullptr, nullptr, 0, 0u);
@@ -1685,6 +1688,8 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
   if (total_chunks == 0) return hipSuccess;
   if (mode == KM_K20)
     full_scatter_kernel<KM_K20><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
+  else if (mode == KM_HASH)
+    full_scatter_kernel<KM_HASH><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
   else
     full_scatter_kernel<KM_GENERIC><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
   return hipGetLastError();
@@ -1700,6 +1705,8 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
                                                                       dchunk, entries, tab, lgR, chunk_first)
   if (mode == KM_K20) {
     if (exact) DLSM_PART(KM_K20, true); else DLSM_PART(KM_K20, false);
+  } else if (mode == KM_HASH) {
+    DLSM_PART(KM_HASH, true);  // hashed jobs always run the count pass first
   } else if (mode == KM_K28) {
     if (exact) DLSM_PART(KM_K28, true); else DLSM_PART(KM_K28, false);
   } else {

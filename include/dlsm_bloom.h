@@ -211,6 +211,38 @@ int dlsm_bloom_full_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_j
 int dlsm_bloom_full_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
                           int bits_per_key, uint64_t* out_len);
 
+/* The same build from BloomHash values instead of keys: each job's keys is a
+ * set of n u32 hashes (key_len 4, offsets NULL, suffix_len 0, 4-byte aligned)
+ * in AddKey order -- FullFilterBlockBuilder::hash_entries_
+ * (full_filter_block.cc:39-49), which a caller that hashes in AddKey on the
+ * host hands over at 4 bytes per key instead of the key bytes.  Consecutive
+ * equal hashes are dropped on the GPU exactly like AddKey's check, so the
+ * hashes may be given deduplicated or not. */
+int dlsm_bloom_full_build_hashed_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                     int bits_per_key, uint64_t* out_len_dev);
+int dlsm_bloom_full_build_hashed(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
+                                 int bits_per_key, uint64_t* out_len);
+
+/* ---- concurrent Finish calls gathered into batched builds --------------- */
+
+/* A per-device submission queue for many builder threads (dLSM runs up to 4
+ * flush + 12 compaction + 12 subcompaction builders at once,
+ * include/TimberSaw/options.h:73-78).  dlsm_batcher_full_build[_hashed] has
+ * dlsm_bloom_full_build[_hashed]'s meaning for ONE job (host keys, host slot)
+ * and blocks until that filter is in the slot; concurrent calls are gathered
+ * into one batched build by `executors` worker threads (each with its own
+ * context and stream) that take every queued job, after waiting up to
+ * window_us (0: no wait) for at most max_jobs.  The job's key bytes and slot
+ * must stay valid until the call returns (page-locked memory: DMA). */
+typedef struct dlsm_batcher dlsm_batcher;
+int dlsm_batcher_create(int device, int executors, uint32_t window_us, uint32_t max_jobs, dlsm_batcher** out);
+int dlsm_batcher_destroy(dlsm_batcher* b);
+int dlsm_batcher_full_build(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, uint64_t* out_len);
+int dlsm_batcher_full_build_hashed(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key,
+                                   uint64_t* out_len);
+/* Batches run, jobs built, and the largest batch so far. */
+int dlsm_batcher_stats(dlsm_batcher* b, uint64_t* batches, uint64_t* jobs, uint64_t* max_batch);
+
 /* FinishFilterBlock (table/table_builder_computeside.cc:389-432): the full
  * filter followed by the 5-byte block trailer [type 0][Fixed32(crc32c::Mask(
  * crc32c(filter || type)))] -- the exact bytes FlushFilter RDMA-writes

@@ -14,4 +14,5 @@ rc=$?
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 python bench.py --gpus 2 --rehearse --steps 20 --warmup 5 > "$OUT/bench_g2r.json" 2> "$OUT/bench_g2r.err" &&
 timeout -k 10 300 python bench.py --gpus 4 --rehearse --steps 20 --warmup 5 > "$OUT/bench_g4r.json" 2> "$OUT/bench_g4r.err" &&
+timeout -k 10 300 python tests/diag/run_scatter_mask.py > "$OUT/scatter_mask.json" 2> "$OUT/scatter_mask.err" &&
 exit $rc
