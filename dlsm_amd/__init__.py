@@ -360,6 +360,28 @@ class Context:
         call.keep = keep
         return call
 
+    def full_build_hashed(self, hash_sets, bits_per_key: int = 10, caps=None) -> list:
+        """Filters from BloomHash values (numpy uint32 arrays, AddKey order;
+        consecutive equal hashes are dropped like AddKey) -- host in/out."""
+        sets = [np.ascontiguousarray(h, dtype=np.uint32) for h in hash_sets]
+        tables = [Keys(h if h.size else np.zeros(1, dtype=np.uint32), h.size, 4) for h in sets]
+        if caps is None:
+            caps = [full_size(h.size, bits_per_key)[0] for h in sets]
+        outs = [np.zeros(max(c, 1), dtype=np.uint8) for c in caps]
+        jobs = self._jobs(tables, outs, caps)
+        n = len(tables)
+        lens = (C.c_uint64 * max(n, 1))()
+        check(lib().dlsm_bloom_full_build_hashed(self.h, jobs, n, bits_per_key, lens), "full_build_hashed")
+        return [outs[j][: lens[j]].tobytes() for j in range(n)]
+
+    def full_build_hashed_dev(self, hash_sets, outs, out_lens, bits_per_key: int = 10):
+        """Device form: hash_sets are device uint32 tensors."""
+        tables = [Keys(h, int(h.numel()), 4) for h in hash_sets]
+        caps = [int(o.numel()) for o in outs]
+        jobs = self._jobs(tables, outs, caps)
+        check(lib().dlsm_bloom_full_build_hashed_dev(self.h, jobs, len(tables), bits_per_key, _ptr(out_lens)),
+              "full_build_hashed_dev")
+
     def full_build_block(self, tables: Sequence[Keys], bits_per_key: int = 10, caps=None) -> list:
         """Filter + 5-byte block trailer (FinishFilterBlock), host in/out."""
         n = len(tables)

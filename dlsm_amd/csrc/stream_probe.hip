@@ -79,9 +79,32 @@ __global__ __launch_bounds__(kNT) void copy_kernel(const u32x4* __restrict__ src
   for (; i < end; i += step) st<NT>(dst + i, ld<NT>(src + i));
 }
 
+// The probe partition's byte shape: 20 B read and 6 B written per key, as a
+// read stream and a write stream of 16-byte units in the ratio 10 : 3.
+template <bool NT, bool CHUNKED>
+__global__ __launch_bounds__(kNT) void part_shape_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                         uint64_t n16) {
+  uint64_t i, end, step;
+  range<CHUNKED>(n16, i, end, step);
+  // this thread's write position: the same walk over a range 3/10 as long
+  uint64_t w = CHUNKED ? (i - threadIdx.x) / 10 * 3 + threadIdx.x : i;
+  for (; i + 9 * step < end; i += 10 * step, w += 3 * step) {
+    u32x4 v[10];
+#pragma unroll
+    for (int u = 0; u < 10; u++) v[u] = ld<NT>(src + i + u * step);
+    const u32x4 a = v[0] ^ v[1] ^ v[2], b = v[3] ^ v[4] ^ v[5], c = v[6] ^ v[7] ^ v[8] ^ v[9];
+    st<NT>(dst + w, a);
+    st<NT>(dst + w + step, b);
+    st<NT>(dst + w + 2 * step, c);
+  }
+}
+
 template <bool NT, bool CHUNKED>
 hipError_t launch(int kind, const void* src, void* dst, uint64_t n16, unsigned blocks, hipStream_t s) {
-  if (kind == 0)
+  if (kind == 2)
+    part_shape_kernel<NT, CHUNKED><<<blocks, kNT, 0, s>>>(static_cast<const u32x4*>(src), static_cast<u32x4*>(dst),
+                                                          n16);
+  else if (kind == 0)
     read_kernel<NT, CHUNKED><<<blocks, kNT, 0, s>>>(static_cast<const u32x4*>(src), n16,
                                                      static_cast<uint32_t*>(dst));
   else
@@ -93,7 +116,7 @@ hipError_t launch(int kind, const void* src, void* dst, uint64_t n16, unsigned b
 
 extern "C" int dlsm_stream_kernel(void* hip_stream, int kind, int variant, const void* src, void* dst,
                                   uint64_t bytes, uint32_t blocks) {
-  if (kind < 0 || kind > 1 || variant < 0 || variant > 3 || !src || !dst || blocks == 0 || (bytes & 15u))
+  if (kind < 0 || kind > 2 || variant < 0 || variant > 3 || !src || !dst || blocks == 0 || (bytes & 15u))
     return DLSM_E_ARG;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) return DLSM_E_ARG;
   const uint64_t n16 = bytes / 16;

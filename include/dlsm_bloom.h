@@ -448,7 +448,9 @@ int dlsm_multi_device_run(const dlsm_device_work* work, int n_devices, int bits_
 /* The box's HBM streaming ceilings for the roofline (bench.py): launch one
  * 16-byte-per-lane streaming kernel on hip_stream over `bytes` (a multiple of
  * 16; 16-byte-aligned buffers).  kind 0: read src (dst receives at most 512
- * u32 of sink writes, normally none); kind 1: copy src -> dst.  variant bit
+ * u32 of sink writes, normally none); kind 1: copy src -> dst; kind 2: the
+ * probe partition's byte shape, reading src and writing 3/10 as many bytes to
+ * dst (20 B in, 6 B out per key).  variant bit
  * 0: non-temporal accesses; bit 1: one contiguous range per workgroup (else
  * grid-stride).  blocks: workgroups of 512 threads.  Asynchronous. */
 int dlsm_stream_kernel(void* hip_stream, int kind, int variant, const void* src, void* dst, uint64_t bytes,

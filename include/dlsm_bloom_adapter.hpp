@@ -88,6 +88,42 @@ inline Slice ExtractUserKey(const Slice& internal_key) {
                                         : 0);
 }
 
+// BloomHash(key) = Hash(key, n, 0xbc9f1d34) (include/TimberSaw/filter_policy.h:
+// 26-28, util/hash.cc:22-62): MurmurHash1-style over little-endian 4-byte
+// words, the 1-3 tail bytes sign-extended.  Inline so AddKey can hash on the
+// host exactly as the reference's AddKey does (the library's
+// dlsm_bloom_hash gives the same value; tests compare them).
+inline uint32_t BloomHash(const char* data, size_t n) {
+  const uint32_t m = 0xc6a4a793u;
+  uint32_t h = 0xbc9f1d34u ^ static_cast<uint32_t>(n * m);
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(data);
+  size_t i = 0;
+  for (; i + 4 <= n; i += 4) {
+    uint32_t w;
+    std::memcpy(&w, p + i, 4);  // x86 / gfx hosts: little-endian, like DecodeFixed32
+    h += w;
+    h *= m;
+    h ^= (h >> 16);
+  }
+  const auto sx = [](unsigned char c) { return static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(c))); };
+  switch (n - i) {
+    case 3:
+      h += sx(p[i + 2]) << 16;
+      [[fallthrough]];
+    case 2:
+      h += sx(p[i + 1]) << 8;
+      [[fallthrough]];
+    case 1:
+      h += sx(p[i]);
+      h *= m;
+      h ^= (h >> 24);
+      break;
+    default:
+      break;
+  }
+  return h;
+}
+
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
 struct FilterSlot {
   void* addr;
@@ -149,11 +185,25 @@ class PinnedBytes {
   bool decided_ = false, shared_ = false;
 };
 
+// How a builder hands its table to the GPU at Finish.
+//  * ctx only: its own context, one synchronous build per table;
+//  * batcher: the device's submission queue (dlsm_batcher): concurrent
+//    Finish calls of many builder threads become one batched build;
+//  * hash_in_addkey: AddKey computes BloomHash and drops a hash equal to
+//    the previous one on the host -- the reference's own AddKey
+//    (full_filter_block.cc:39-49) -- so Finish moves 4 bytes per distinct
+//    key over PCIe instead of the key bytes, and the GPU builds from the
+//    hashes (dlsm_bloom_full_build_hashed).  Same filter bytes either way.
+struct BuilderOptions {
+  dlsm_batcher* batcher = nullptr;
+  bool hash_in_addkey = false;
+};
+
 class FullFilterBlockBuilder {
  public:
-  FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx)
+  FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx, BuilderOptions opt = {})
       : local_mr_(mr), bits_per_key_(bits_per_key),
-        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx), keys_(ctx),
+        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx), opt_(opt), keys_(ctx),
         result(static_cast<char*>(mr->addr), 0) {}
   FullFilterBlockBuilder(const FullFilterBlockBuilder&) = delete;
   FullFilterBlockBuilder& operator=(const FullFilterBlockBuilder&) = delete;
@@ -167,6 +217,18 @@ class FullFilterBlockBuilder {
   // the line count is counted exactly before bucketing: DLSM_OPT_BUILD_EXACT).
   void AddKey(const Slice& key) {
     if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
+    if (opt_.hash_in_addkey) {
+      const uint32_t h = BloomHash(key.data(), key.size());
+      if (n_ == 0 || h != last_hash_) {  // full_filter_block.cc:45-48
+        if (!keys_.append(reinterpret_cast<const char*>(&h), 4)) {
+          stage_status_ = DLSM_E_NOMEM;
+          return;
+        }
+        last_hash_ = h;
+        n_++;
+      }
+      return;
+    }
     const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
     if (n_ == 0) {
       key_len_ = key.size();
@@ -199,7 +261,10 @@ class FullFilterBlockBuilder {
     job.keys.bytes = keys_.data();
     job.keys.n = n_;
     job.keys.suffix_len = 0;
-    if (uniform_) {
+    if (opt_.hash_in_addkey) {  // BloomHash values, already deduplicated
+      job.keys.offsets = nullptr;
+      job.keys.key_len = 4;
+    } else if (uniform_) {
       job.keys.offsets = nullptr;
       job.keys.key_len = static_cast<uint32_t>(key_len_);
     } else {
@@ -213,12 +278,19 @@ class FullFilterBlockBuilder {
     // first (this builder's context belongs to its thread; the caller's
     // setting is restored after the call)
     uint64_t exact = 0;
-    if (dups_) {
+    if (dups_ && ctx_) {
       dlsm_ctx_get_option(ctx_, DLSM_OPT_BUILD_EXACT, &exact);
       dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 1);
     }
-    status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
-    if (dups_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
+    if (opt_.batcher && opt_.hash_in_addkey)
+      status_ = dlsm_batcher_full_build_hashed(opt_.batcher, &job, bits_per_key_, &len);
+    else if (opt_.batcher)  // the batcher's own contexts count exactly when told
+      status_ = dlsm_batcher_full_build(opt_.batcher, &job, bits_per_key_, &len);
+    else if (opt_.hash_in_addkey)
+      status_ = dlsm_bloom_full_build_hashed(ctx_, &job, 1, bits_per_key_, &len);
+    else
+      status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
+    if (dups_ && ctx_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
     clear_keys();
     result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
@@ -258,7 +330,9 @@ class FullFilterBlockBuilder {
   int bits_per_key_;
   int num_probes_;
   dlsm_ctx* ctx_;
-  PinnedBytes keys_;               // the keys, back to back
+  BuilderOptions opt_;
+  PinnedBytes keys_;               // the keys back to back, or their BloomHash values
+  uint32_t last_hash_ = 0;         // hash_in_addkey: the last staged hash
   std::vector<uint64_t> offsets_;  // key boundaries, only once lengths differ
   bool uniform_ = true;
   size_t key_len_ = 0, last_len_ = 0;

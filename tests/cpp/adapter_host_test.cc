@@ -29,6 +29,21 @@ int main() {
   CHECK(b.output_capacity() == other.size());
   b.Reset();                                   // back to the slot (full_filter_block.cc:141-143)
   CHECK(b.output_capacity() == slot.size());
+  // the header's inline BloomHash (AddKey's host hashing) == the library's,
+  // lengths 0..70 with bytes >= 0x80 in every tail position (sign extension)
+  {
+    std::vector<char> k(70);
+    uint32_t x = 12345u;
+    for (int rep = 0; rep < 40; rep++) {
+      for (auto& c : k) {
+        x = x * 1664525u + 1013904223u;
+        c = static_cast<char>(x >> 24);
+      }
+      for (size_t n = 0; n <= k.size(); n++)
+        CHECK(dlsm_adapter::BloomHash(k.data(), n) == dlsm_bloom_hash(k.data(), n));
+    }
+    CHECK(dlsm_adapter::BloomHash("\xc3\x97", 2) == 0x0f2ba540u);  // the reference code's value
+  }
   // the staging-buffer claim needs a context
   CHECK(dlsm_ctx_host_buffer_claim(nullptr, &b) == DLSM_E_ARG);
   CHECK(dlsm_ctx_host_buffer_release(nullptr, &b) == DLSM_E_ARG);

@@ -15,7 +15,14 @@
 // context allocates device memory after its warm-up table (dlsm_ctx_stats);
 // prints per-Finish latency and both aggregate rates as one JSON line.
 //
-//   concurrent_builders [threads=16] [tables_per_thread=8] [keys=153846]
+//   concurrent_builders [threads=16] [tables_per_thread=8] [keys=153846] [mode=ctx]
+//
+// mode: ctx        -- one dlsm_ctx per thread, one synchronous build per table;
+//       batch      -- Finish goes through the device's dlsm_batcher: the
+//                     threads' concurrent calls become batched builds;
+//       hash       -- one ctx per thread, AddKey hashes on the host (the
+//                     reference's AddKey) and Finish sends 4 B per key;
+//       batch-hash -- both.
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -71,9 +78,10 @@ struct ThreadResult {
   Clock::time_point gpu_start, gpu_end, cpu_start, cpu_end;
 };
 
-static void run_thread(int t, int threads, int tables, int n, Barrier* bar, ThreadResult* r) {
+static void run_thread(int t, int threads, int tables, int n, Barrier* bar, ThreadResult* r,
+                       dlsm_adapter::BuilderOptions opt) {
   dlsm_ctx* ctx = nullptr;
-  const int ok_ctx = dlsm_ctx_create(0, &ctx);
+  const int ok_ctx = opt.batcher ? DLSM_OK : dlsm_ctx_create(0, &ctx);
   uint64_t spec = 0;
   dlsm_bloom_full_size(n, 10, nullptr, &spec);
   const size_t slot_len = 256 * 1024 > spec ? 256 * 1024 : spec;  // FilterChunk slot (options.h:28)
@@ -93,7 +101,7 @@ static void run_thread(int t, int threads, int tables, int n, Barrier* bar, Thre
   dlsm_adapter::FilterSlot mr{slot_mem, slot_len};
   auto build = [&](int q, bool timed) {
     if (r->failures) return;
-    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx);
+    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx, opt);
     std::memset(slot_mem, 0, slot_len);  // Rep ctor memsets the slot (table_builder_computeside.cc:38)
     const auto t0 = Clock::now();
     b.RestartBlock(0);
@@ -115,11 +123,11 @@ static void run_thread(int t, int threads, int tables, int n, Barrier* bar, Thre
   };
   bar->wait();
   build(0, false);  // warm-up
-  if (!r->failures) dlsm_ctx_stats(ctx, &r->allocs_after_warmup, nullptr);
+  if (!r->failures && ctx) dlsm_ctx_stats(ctx, &r->allocs_after_warmup, nullptr);
   r->gpu_start = bar->wait();
   for (int q = 1; q <= tables; q++) build(q, true);
   r->gpu_end = Clock::now();
-  if (!r->failures) dlsm_ctx_stats(ctx, &r->allocs_end, nullptr);
+  if (!r->failures && ctx) dlsm_ctx_stats(ctx, &r->allocs_end, nullptr);
   std::vector<std::vector<uint8_t>> want(tables + 1, std::vector<uint8_t>(spec));
   std::vector<int64_t> wl(tables + 1);
   r->cpu_start = bar->wait();
@@ -141,11 +149,30 @@ int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 16;
   const int tables = argc > 2 ? std::atoi(argv[2]) : 8;
   const int n = argc > 3 ? std::atoi(argv[3]) : 153846;
+  const std::string mode = argc > 4 ? argv[4] : "ctx";
+  dlsm_adapter::BuilderOptions opt;
+  opt.hash_in_addkey = mode == "hash" || mode == "batch-hash";
+  dlsm_batcher* batcher = nullptr;
+  if (mode == "batch" || mode == "batch-hash") {
+    if (dlsm_batcher_create(0, 2, 0, 64, &batcher) != DLSM_OK) {
+      std::printf("FAIL batcher_create\n");
+      return 1;
+    }
+    opt.batcher = batcher;
+  } else if (mode != "ctx" && mode != "hash") {
+    std::printf("FAIL unknown mode %s\n", mode.c_str());
+    return 1;
+  }
   std::vector<ThreadResult> res(threads);
   Barrier bar(threads);
   std::vector<std::thread> th;
-  for (int t = 0; t < threads; t++) th.emplace_back(run_thread, t, threads, tables, n, &bar, &res[t]);
+  for (int t = 0; t < threads; t++) th.emplace_back(run_thread, t, threads, tables, n, &bar, &res[t], opt);
   for (auto& x : th) x.join();
+  uint64_t nb = 0, nj = 0, mb = 0;
+  if (batcher) {
+    dlsm_batcher_stats(batcher, &nb, &nj, &mb);
+    dlsm_batcher_destroy(batcher);
+  }
   int fails = 0;
   std::vector<double> lat;
   double add_ms = 0;
@@ -168,12 +195,14 @@ int main(int argc, char** argv) {
   const double gpu_ms = std::chrono::duration<double, std::milli>(ge - gs).count();
   const double cpu_ms = std::chrono::duration<double, std::milli>(ce - cs).count();
   std::printf(
-      "{\"threads\": %d, \"tables_per_thread\": %d, \"keys_per_table\": %d, \"failures\": %d, "
+      "{\"mode\": \"%s\", \"batches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu, "
+      "\"threads\": %d, \"tables_per_thread\": %d, \"keys_per_table\": %d, \"failures\": %d, "
       "\"no_device_alloc_after_warmup\": %s, \"finish_ms\": {\"median\": %.4f, \"p90\": %.4f, \"p99\": %.4f, "
       "\"max\": %.4f, \"mean\": %.4f}, \"addkey_ns_per_key\": %.2f, "
       "\"gpu_adapter\": {\"wall_ms\": %.2f, \"mkeys_s\": %.1f, \"tables_per_s\": %.0f}, "
       "\"cpu_oracle_same_threads\": {\"wall_ms\": %.2f, \"mkeys_s\": %.1f, \"ms_per_table\": %.3f}}\n",
-      threads, tables, n, fails, no_alloc ? "true" : "false", pct(0.5), pct(0.9), pct(0.99),
+      mode.c_str(), static_cast<unsigned long long>(nb), nb ? static_cast<double>(nj) / nb : 0.0,
+      static_cast<unsigned long long>(mb), threads, tables, n, fails, no_alloc ? "true" : "false", pct(0.5), pct(0.9), pct(0.99),
       lat.empty() ? 0.0 : lat.back(), lat.empty() ? 0.0 : sum / lat.size(),
       add_ms * 1e6 / keys_timed, gpu_ms, keys_timed / (gpu_ms * 1e3), threads * tables / (gpu_ms * 1e-3),
       cpu_ms, keys_timed / (cpu_ms * 1e3), cpu_ms * threads / (threads * tables));

@@ -91,3 +91,19 @@ def test_sixteen_concurrent_builder_threads(tmp_path):
     rec = json.loads(out.stdout.splitlines()[0])
     assert rec["failures"] == 0 and rec["no_device_alloc_after_warmup"]
     print(json.dumps(rec))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["batch", "hash", "batch-hash"])
+def test_concurrent_builders_batched_and_hashed(tmp_path, mode):
+    """The same 16-thread call shape with Finish through the device's batcher
+    (concurrent calls -> batched builds) and/or AddKey hashing on the host (4 B
+    per key over PCIe): every filter equals the oracle's."""
+    exe = _compile(tmp_path, "concurrent_builders")
+    out = subprocess.run([str(exe), "16", "3", "153846", mode], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0 and "OK concurrent builders" in out.stdout, out.stdout + out.stderr
+    rec = json.loads(out.stdout.splitlines()[0])
+    assert rec["failures"] == 0 and rec["mode"] == mode
+    if mode.startswith("batch"):
+        assert rec["batches"] >= 1 and rec["max_batch"] >= 1
+    print(json.dumps(rec))
