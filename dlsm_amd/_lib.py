@@ -86,6 +86,9 @@ SIGNATURES = [
     ("dlsm_host_unregister", C.c_int, [_VP]),
     ("dlsm_host_alloc", C.c_int, [C.c_size_t, C.POINTER(_VP)]),
     ("dlsm_host_free", C.c_int, [_VP]),
+    ("dlsm_host_pool_acquire", C.c_int, [C.c_uint64, C.POINTER(_VP), _U64P]),
+    ("dlsm_host_pool_release", C.c_int, [_VP]),
+    ("dlsm_host_pool_trim", C.c_int, []),
     ("dlsm_ctx_host_buffer_claim", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_host_buffer_release", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_host_buffer", C.c_int, [_VP, C.c_uint64, C.c_uint64, C.POINTER(_VP), _U64P]),

@@ -5,6 +5,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <unordered_map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -620,6 +623,72 @@ int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes,
   return DLSM_OK;
 }
 
+// Process-wide pool of page-locked host buffers (key staging of builders
+// that cannot borrow their context's buffer): a released buffer is kept and
+// handed to the next acquire that fits, so steady-state staging page-locks
+// nothing.  Sizes are powers of two >= 1 MiB.
+}  // extern "C"
+namespace {
+struct HostPool {
+  std::mutex m;
+  std::multimap<uint64_t, void*> free_by_size;
+  std::unordered_map<void*, uint64_t> size_of;
+};
+HostPool& host_pool() {
+  static HostPool p;
+  return p;
+}
+}  // namespace
+extern "C" {
+
+int dlsm_host_pool_acquire(uint64_t min_bytes, void** out, uint64_t* cap) {
+  if (!out) return DLSM_E_ARG;
+  *out = nullptr;
+  HostPool& hp = host_pool();
+  {
+    std::lock_guard<std::mutex> lk(hp.m);
+    auto it = hp.free_by_size.lower_bound(min_bytes);
+    if (it != hp.free_by_size.end()) {
+      *out = it->second;
+      if (cap) *cap = it->first;
+      hp.free_by_size.erase(it);
+      return DLSM_OK;
+    }
+  }
+  uint64_t c = uint64_t(1) << 20;
+  while (c < min_bytes) c <<= 1;
+  void* p = nullptr;
+  DLSM_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
+  {
+    std::lock_guard<std::mutex> lk(hp.m);
+    hp.size_of[p] = c;
+  }
+  *out = p;
+  if (cap) *cap = c;
+  return DLSM_OK;
+}
+
+int dlsm_host_pool_release(void* p) {
+  if (!p) return DLSM_OK;
+  HostPool& hp = host_pool();
+  std::lock_guard<std::mutex> lk(hp.m);
+  auto it = hp.size_of.find(p);
+  if (it == hp.size_of.end()) return DLSM_E_ARG;
+  hp.free_by_size.emplace(it->second, p);
+  return DLSM_OK;
+}
+
+int dlsm_host_pool_trim(void) {
+  HostPool& hp = host_pool();
+  std::lock_guard<std::mutex> lk(hp.m);
+  for (auto& kv : hp.free_by_size) {
+    (void)hipHostFree(kv.second);
+    hp.size_of.erase(kv.second);
+  }
+  hp.free_by_size.clear();
+  return DLSM_OK;
+}
+
 int dlsm_host_alloc(size_t len, void** out) {
   if (!out || !len) return DLSM_E_ARG;
   *out = nullptr;
@@ -1216,24 +1285,41 @@ int dlsm_filterset_size(const dlsm_filterset* fs, int* n_filters, uint64_t* devi
 
 namespace {
 
-// Slices of 2^lgR image lines for a group of line count L (a byte-wide
-// stacked table with more than kMaxSlices slices of 64 KiB moves to 128 KiB
-// slices, one workgroup per CU; packed images always use 128 KiB slices of
-// 2^(11 - lgw) lines); 0 when the group cannot be sliced.
-uint32_t group_slices(const dlsm_ctx* ctx, const ProbeGroup& g, int* lgR) {
+// Slices of a group's image (line count L): the LDS holds up to 2^lgR lines
+// (a byte-wide stacked table with more than kMaxSlices slices of 64 KiB moves
+// to 128 KiB, one workgroup per CU; packed images always use 128 KiB of
+// 2^(11 - lgw) lines).  Balanced: the slice pass runs S x parts workgroups
+// with parts = 256 / S0 (slice_parts, S0 = the slice count at full width),
+// so the slices are narrowed to R = ceil(L / floor(256 / parts)) lines to fill
+// the 256 CUs exactly -- 8 x 1.6 M-key filters (31,251 lines): 128 slices of
+// 245 lines x 2 parts = 256 workgroups instead of 123 x 2 = 246.
+// ($DLSM_PROBE_BALANCE=0: full-width slices, for A/B.)  Returns S, or 0
+// when the group cannot be sliced.
+uint32_t group_slices(const dlsm_ctx* ctx, const ProbeGroup& g, int* lgR, uint32_t* R_out) {
+  static const bool balance = [] {
+    const char* e = getenv("DLSM_PROBE_BALANCE");
+    return !(e && atoi(e) == 0);
+  }();
   const uint32_t L = g.L;
   if (g.lgw < 3) {
     *lgR = 11 - g.lgw;
-    const uint32_t S = ceil_div_u32(L, 1u << *lgR);
-    return S >= 1 && S <= kMaxSlices ? S : 0;
+  } else {
+    *lgR = ctx->probe_lgr;
+    if (ceil_div_u32(L, 1u << *lgR) > kMaxSlices && *lgR < 8) *lgR = 8;
   }
-  *lgR = ctx->probe_lgr;
-  uint32_t S = ceil_div_u32(L, 1u << *lgR);
-  if (S > kMaxSlices && *lgR < 8) {
-    *lgR = 8;
-    S = ceil_div_u32(L, 1u << *lgR);
+  const uint32_t Rmax = 1u << *lgR;
+  const uint32_t S0 = ceil_div_u32(L, Rmax);
+  if (S0 < 1 || S0 > kMaxSlices) return 0;
+  uint32_t R = Rmax;
+  const uint32_t per_cu = *lgR == 7 && g.lgw == 3 ? 2u : 1u;  // slice workgroups resident per CU
+  const uint32_t slots = kBuildSliceCUs * per_cu;
+  if (balance && S0 < slots) {
+    const uint32_t parts = std::max(1u, slots / S0);
+    const uint32_t S_target = slots / parts;
+    R = std::min(Rmax, ceil_div_u32(L, S_target));
   }
-  return S >= 1 && S <= kMaxSlices ? S : 0;
+  *R_out = R;
+  return ceil_div_u32(L, R);
 }
 
 // (slice, part) workgroups of the slice pass: about one resident wave of
@@ -1273,7 +1359,8 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   uint32_t Smax = 0;
   for (const auto& g : fs->groups) {
     int lg;
-    Smax = std::max(Smax, group_slices(ctx, g, &lg));
+    uint32_t R;
+    Smax = std::max(Smax, group_slices(ctx, g, &lg, &R));
   }
   const uint64_t rstride = static_cast<uint64_t>(nC) * probe_region(static_cast<uint32_t>(C));
   DLSM_CHECK(ctx->entries.ensure(rstride));
@@ -1283,15 +1370,16 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   for (size_t gi = 0; gi < fs->groups.size(); gi++) {
     const ProbeGroup& g = fs->groups[gi];
     int lgR;
-    const uint32_t S = group_slices(ctx, g, &lgR);
+    uint32_t R;
+    const uint32_t S = group_slices(ctx, g, &lgR, &R);
     if (S == 0 || ctx->path == 1) {
       DLSM_TRY(launch_probe_direct_group(fs->d_slots + 8 * gi, hk, mask_dev, mb, g.mask_byte,
                                          g.first_of_byte, s));
       continue;
     }
-    DLSM_TRY(launch_probe_partition(hk, g.L, g.magic, lgR, S, ctx->entries.p, ctx->pos.p, ctx->tab.p,
+    DLSM_TRY(launch_probe_partition(hk, g.L, g.magic, R, S, ctx->entries.p, ctx->pos.p, ctx->tab.p,
                                     KM_HASH, lgC, s));
-    DLSM_TRY(launch_probe_slices(g.stacked, g.L, g.magic, g.k, lgR, g.lgw, g.slotmap, S, nC, ctx->entries.p,
+    DLSM_TRY(launch_probe_slices(g.stacked, g.L, g.magic, g.k, lgR, R, g.lgw, g.slotmap, S, nC, ctx->entries.p,
                                  ctx->tab.p, ctx->smask.p, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute_group(n, ctx->pos.p, ctx->smask.p, mask_dev, mb, g.mask_byte,
                                           g.first_of_byte, lgC, s));
@@ -1319,7 +1407,8 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   bool all_sliceable = !fs->groups.empty();
   for (const auto& grp : fs->groups) {
     int lg;
-    all_sliceable = all_sliceable && group_slices(ctx, grp, &lg) != 0;
+    uint32_t R;
+    all_sliceable = all_sliceable && group_slices(ctx, grp, &lg, &R) != 0;
   }
   if (ctx->path == 2 && !(all_sliceable && fits)) return DLSM_E_ARG;
   if (fs->groups.empty() || ctx->path == 1 || !fits) {
@@ -1332,7 +1421,8 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   // hashed inside the partition pass.
   const ProbeGroup& grp = fs->groups[0];
   int lgR;
-  const uint32_t S = group_slices(ctx, grp, &lgR);
+  uint32_t R;
+  const uint32_t S = group_slices(ctx, grp, &lgR, &R);
   // Rounds of probe_round keys, pipelined: round r's partition (helper
   // stream) overlaps round r-1's slice + unpermute (context stream), or
   // serial (DLSM_OPT_PROBE_ROUND_SERIAL).  A round's intermediates (4 B hash +
@@ -1374,11 +1464,11 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     if (kd.offsets) kr.offsets = kd.offsets + r0;
     else kr.bytes = kd.bytes + r0 * kd.key_len;
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
-    DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, lgR, S, ent, pos, tab, mode, lgC, ps,
+    DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, R, S, ent, pos, tab, mode, lgC, ps,
                                     split ? ctx->pcus : 0u));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
     if (split) DLSM_CHECK(join_part(ctx));
-    DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, grp.lgw, grp.slotmap, S, nC, ent,
+    DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, R, grp.lgw, grp.slotmap, S, nC, ent,
                                  tab, sm, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));

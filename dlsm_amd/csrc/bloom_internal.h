@@ -154,14 +154,16 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
                                         hipStream_t s);
 // lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice
 // (7, 8 for byte-wide stacked images; 11 - lgw for packed ones, lgw < 3).
-hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
+// R: filter lines per slice (<= 256 for byte images, 2^(11-lgw) for packed).
+hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                   uint16_t* tab, int mode, int lgC, hipStream_t s,
                                   uint32_t cus = 0);  // CUs the persistent grid is sized for (0: the device's)
 // lgw 3: byte-wide stacked image (launch_stack_filters); lgw 0..2: packed
 // image (launch_pack_filters) whose member m answers in bit (slotmap >> 4m) & 7.
+// lgR: log2 of the LDS capacity in lines; R <= 2^lgR: the slice size in lines.
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
-                               int lgR, int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
+                               int lgR, uint32_t R, int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
                                int parts, int lgC, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,

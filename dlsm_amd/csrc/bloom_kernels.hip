@@ -1161,7 +1161,7 @@ __device__ __forceinline__ void for_buckets(uint32_t n, F f) {
 // leave them in the Infinity Cache for a round-sized batch to re-read.
 template <int MODE, int NT, int C, int H = 1, bool NTS = true>
 __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partition_kernel(
-    KeyDesc kd, uint32_t L, uint32_t magic, int lgR, uint32_t S, uint32_t nC,
+    KeyDesc kd, uint32_t L, uint32_t magic, uint32_t R, uint32_t rmagic, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
   // H > 1: the chunk is hashed and bucketed in H units of CH keys (the tile
   // pipeline's unit stays CH), ranks keep counting across units, so every
@@ -1238,10 +1238,11 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
         const uint32_t i = static_cast<uint32_t>(u) * CH + il;
         if (il < nku) {
           const uint32_t line = fastmod(h[r], L, magic);
-          const uint32_t sl = line >> lgR;
+          uint32_t off;  // slices of R lines (not a power of two when balanced over the CUs)
+          const uint32_t sl = fastdivmod(line, R, rmagic, &off);
           sb[i] = static_cast<uint8_t>(sl);
           rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
-          h[r] = probe_entry(h[r], line & ((1u << lgR) - 1u));
+          h[r] = probe_entry(h[r], off);
           if (u + 1 < H) park[i] = h[r];
         }
       }
@@ -1323,9 +1324,11 @@ __device__ __forceinline__ uint32_t packed_answer(uint32_t acc, uint32_t slotmap
 // in bit (slotmap >> 4m) & 7.
 template <int LGR, int LGW, int K, int NT, int C>
 __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
-    const uint8_t* __restrict__ stacked, uint32_t L, uint32_t slotmap, int k, uint32_t S,
+    const uint8_t* __restrict__ stacked, uint32_t L, uint32_t Rs, uint32_t slotmap, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts) {
+  // LDS holds up to R = 2^LGR lines; a slice is Rs <= R lines (Rs < R when the
+  // slices are balanced so that S x parts fills the CUs exactly)
   constexpr uint32_t R = 1u << LGR;
   constexpr uint32_t LB = 64u << LGW;  // bytes per line of the image
   static_assert(LGW == 3 || LGR + LGW == 11, "packed images use 128 KiB slices");
@@ -1340,8 +1343,8 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
   const uint32_t s = wi % S;
   const uint32_t p = wi / S;
-  const uint32_t lo_line = s << LGR;
-  const uint32_t nl = min(R, L - lo_line);
+  const uint32_t lo_line = s * Rs;
+  const uint32_t nl = min(Rs, L - lo_line);
   {
     // all of the slice's 16-byte loads in flight before the first LDS store.
     // Loads AND stores are clamped (lanes past the slice rewrite its last
@@ -1886,7 +1889,7 @@ static uint32_t device_cus() {
 // Probe chunk shapes: C keys per partition workgroup of NT threads.
 //   lgC 12: C = 4096, 512 threads;  13: 8192, 1024;  14: 16384, 1024.
 template <int C, int NT, int H = 1>
-static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
+static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                      uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                      uint16_t* tab, int mode, hipStream_t s, uint32_t cus) {
   const uint32_t nC = static_cast<uint32_t>((keys.n + C - 1) / C);
@@ -1905,63 +1908,64 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, i
     return e && atoi(e) != 0;
   }();
   if (mode == KM_HASH)
-    probe_partition_kernel<KM_HASH, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_HASH, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                            entries, pos, tab);
   else if (mode == KM_K20 && plain)
-    probe_partition_kernel<KM_K20, NT, C, H, false><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K20, NT, C, H, false><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                                  entries, pos, tab);
   else if (mode == KM_K20)
-    probe_partition_kernel<KM_K20, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K20, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                           entries, pos, tab);
   else if (mode == KM_K28)
-    probe_partition_kernel<KM_K28, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_K28, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                           entries, pos, tab);
   else
-    probe_partition_kernel<KM_GENERIC, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, lgR, n_slices, nC,
+    probe_partition_kernel<KM_GENERIC, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                               entries, pos, tab);
   return hipGetLastError();
 }
 
-hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, int lgR,
+hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                   uint16_t* tab, int mode, int lgC, hipStream_t s, uint32_t cus) {
   switch (lgC) {
-    case 12: return probe_partition_as<4096, 512>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
+    case 12: return probe_partition_as<4096, 512>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #if DLSM_PROBE_P13_HALF
     // 512-thread workgroups of two 4,096-key units (two resident per CU)
-    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
+    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #else
-    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
+    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #endif
     // 16,384-key chunks bucketed as two 8,192-key units (DLSM_PROBE_UNITS14)
-    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, lgR, n_slices, entries, pos, tab, mode, s, cus);
+    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
     default: return hipErrorInvalidValue;
   }
 }
 
 template <int LGR, int LGW, int C>
-static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t slotmap, int k,
+static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t R, uint32_t slotmap, int k,
                                   uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
                                   const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stacked);
   constexpr int NT = DLSM_PROBE_NT;
+  if (R == 0 || R > (1u << LGR)) return hipErrorInvalidValue;
   if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
     probe_slice_kernel<LGR, LGW, 6, NT, C><<<n_slices * parts, NT, 0, s>>>(
-        st, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
+        st, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
   else
     probe_slice_kernel<LGR, LGW, 0, NT, C><<<n_slices * parts, NT, 0, s>>>(
-        st, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
+        st, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
   return hipGetLastError();
 }
 
-hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR, int lgw,
-                               uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
+hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR, uint32_t R,
+                               int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask, int parts,
                                int lgC, hipStream_t s) {
   (void)magic;  // the partition already reduced every hash to its slice and line
   if (n_chunks == 0) return hipSuccess;
 #define DLSM_SLICES(LG, LW, CC) \
-  return probe_slices_as<LG, LW, CC>(stacked, L, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts, s)
+  return probe_slices_as<LG, LW, CC>(stacked, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts, s)
 #define DLSM_SLICES_C(LG, LW)                  \
   do {                                         \
     if (lgC == 12) DLSM_SLICES(LG, LW, 4096);  \

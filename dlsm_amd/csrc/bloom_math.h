@@ -81,6 +81,23 @@ DLSM_HD uint32_t fastmod(uint32_t h, uint32_t d, uint32_t magic) {
   return r >= d ? r - d : r;
 }
 
+// Quotient and remainder of h by d with the same magic (fastmod_magic(d)):
+// q = mulhi(h, magic) is the true quotient or one less.
+DLSM_HD uint32_t fastdivmod(uint32_t h, uint32_t d, uint32_t magic, uint32_t* rem) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t q = __umulhi(h, magic);
+#else
+  uint32_t q = static_cast<uint32_t>((static_cast<uint64_t>(h) * magic) >> 32);
+#endif
+  uint32_t r = h - q * d;
+  if (r >= d) {
+    r -= d;
+    q++;
+  }
+  *rem = r;
+  return q;
+}
+
 // util/bloom_impl.h:351-357 (full filter, int cast) -- host only (double).
 inline int full_num_probes(int bits_per_key) {
   int k = static_cast<int>(bits_per_key * 0.69);

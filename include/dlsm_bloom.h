@@ -183,6 +183,13 @@ int dlsm_host_unregister(void* p);
  * run as DMA at the link rate). */
 int dlsm_host_alloc(size_t len, void** out);
 int dlsm_host_free(void* p);
+/* A process-wide pool of page-locked host buffers: acquire returns a buffer
+ * of at least min_bytes (*cap: its size), reusing a released one when one
+ * fits; release returns it to the pool (only pool buffers); trim frees every
+ * buffer in the pool.  For key staging of builders that share no context. */
+int dlsm_host_pool_acquire(uint64_t min_bytes, void** out, uint64_t* cap);
+int dlsm_host_pool_release(void* p);
+int dlsm_host_pool_trim(void);
 /* The context's own page-locked host staging buffer, lent to ONE user at a
  * time (the reference runs one TableBuilder per thread, one context per
  * thread): claim returns DLSM_OK when the buffer is free or already held by

@@ -143,7 +143,7 @@ class PinnedBytes {
   PinnedBytes& operator=(const PinnedBytes&) = delete;
   ~PinnedBytes() {
     if (shared_) dlsm_ctx_host_buffer_release(ctx_, this);
-    else if (p_) dlsm_host_free(p_);
+    else if (p_) dlsm_host_pool_release(p_);
   }
   bool append(const char* d, size_t n) {
     if (size_ + n > cap_ && !grow(size_ + n)) return false;
@@ -170,11 +170,13 @@ class PinnedBytes {
       cap_ = c;
       return true;
     }
-    size_t c = cap_ ? 2 * cap_ : (size_t(1) << 20);
-    if (c < need) c = need;
-    if (dlsm_host_alloc(c, &q) != DLSM_OK) return false;
+    // a private buffer from the library's page-locked pool (builders created
+    // per SSTable recycle them: no page-locking after the first tables)
+    uint64_t c = 0;
+    const size_t want = need > 2 * cap_ ? need : 2 * cap_;
+    if (dlsm_host_pool_acquire(want > (size_t(1) << 20) ? want : (size_t(1) << 20), &q, &c) != DLSM_OK) return false;
     if (size_) memcpy(q, p_, size_);
-    if (p_) dlsm_host_free(p_);
+    if (p_) dlsm_host_pool_release(p_);
     p_ = static_cast<uint8_t*>(q);
     cap_ = c;
     return true;
@@ -229,11 +231,12 @@ class FullFilterBlockBuilder {
       }
       return;
     }
-    const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
+    // the previous key is compared from a host copy: page-locked staging may
+    // be mapped uncached for the CPU, so it is written, never read back
     if (n_ == 0) {
       key_len_ = key.size();
     } else {
-      if (key.size() == last_len_ && memcmp(keys_.data() + prev0, key.data(), last_len_) == 0) dups_++;
+      if (key.size() == last_key_.size() && memcmp(last_key_.data(), key.data(), key.size()) == 0) dups_++;
       if (uniform_ && key.size() != key_len_) {  // first key of another length: offsets from now on
         uniform_ = false;
         offsets_.resize(n_ + 1);
@@ -245,7 +248,7 @@ class FullFilterBlockBuilder {
       return;
     }
     if (!uniform_) offsets_.push_back(keys_.size());
-    last_len_ = key.size();
+    last_key_.assign(key.data(), key.size());
     n_++;
   }
   // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
@@ -322,7 +325,8 @@ class FullFilterBlockBuilder {
     keys_.clear();
     offsets_.clear();
     uniform_ = true;
-    key_len_ = last_len_ = 0;
+    key_len_ = 0;
+    last_key_.clear();
     n_ = dups_ = 0;
     stage_status_ = DLSM_OK;
   }
@@ -335,7 +339,8 @@ class FullFilterBlockBuilder {
   uint32_t last_hash_ = 0;         // hash_in_addkey: the last staged hash
   std::vector<uint64_t> offsets_;  // key boundaries, only once lengths differ
   bool uniform_ = true;
-  size_t key_len_ = 0, last_len_ = 0;
+  size_t key_len_ = 0;
+  std::string last_key_;           // the previous key (AddKey's duplicate check)
   uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = 0;
   int status_ = DLSM_OK;        // the last Finish's result

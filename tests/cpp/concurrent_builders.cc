@@ -15,7 +15,7 @@
 // context allocates device memory after its warm-up table (dlsm_ctx_stats);
 // prints per-Finish latency and both aggregate rates as one JSON line.
 //
-//   concurrent_builders [threads=16] [tables_per_thread=8] [keys=153846] [mode=ctx]
+//   concurrent_builders [threads=16] [tables_per_thread=8] [keys=153846] [mode=ctx] [window_us=0]
 //
 // mode: ctx        -- one dlsm_ctx per thread, one synchronous build per table;
 //       batch      -- Finish goes through the device's dlsm_batcher: the
@@ -154,7 +154,8 @@ int main(int argc, char** argv) {
   opt.hash_in_addkey = mode == "hash" || mode == "batch-hash";
   dlsm_batcher* batcher = nullptr;
   if (mode == "batch" || mode == "batch-hash") {
-    if (dlsm_batcher_create(0, 2, 0, 64, &batcher) != DLSM_OK) {
+    const uint32_t window_us = argc > 5 ? static_cast<uint32_t>(std::atoi(argv[5])) : 0u;
+    if (dlsm_batcher_create(0, 2, window_us, 64, &batcher) != DLSM_OK) {
       std::printf("FAIL batcher_create\n");
       return 1;
     }
