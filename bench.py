@@ -101,6 +101,9 @@ def main():
                     help="1: capture one step (build + probe launches) in a HIP graph and replay it")
     ap.add_argument("--rehearse", action="store_true",
                     help="--gpus N in one process on a box with fewer GPUs: N logical devices on GPU 0")
+    ap.add_argument("--native", action="store_true",
+                    help="time the steps with the library's native runner (dlsm_multi_device_run) at any N "
+                         "(the default for --gpus N > 1; at N = 1 the Python loop is the default)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
@@ -113,7 +116,7 @@ def main():
         log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}: launch one rank per GPU "
             f"(--nproc-per-node {args.gpus}) or drop the launcher")
         sys.exit(2)
-    if env_world is None and args.gpus > 1:
+    if env_world is None and (args.gpus > 1 or args.native):
         sys.exit(run_threads(args))
     if args.rehearse and args.gpus == 1 and env_world is None:
         log("bench.py: --rehearse only applies to --gpus N > 1")
@@ -371,8 +374,9 @@ def main():
 
 
 def run_threads(args) -> int:
-    """--gpus N > 1 in one process: a host thread + dlsm_ctx + stream per GPU
-    (dlsm_amd/multigpu.py), strong scaling of config 4.  Returns the exit code."""
+    """--gpus N in one process: a host thread + dlsm_ctx + stream per GPU
+    (dlsm_amd/multigpu.py) timed by the native runner, strong scaling of
+    config 4 (N = 1 with --native).  Returns the exit code."""
     import numpy as np
     import torch
 

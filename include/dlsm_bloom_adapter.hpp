@@ -97,6 +97,16 @@ inline uint32_t BloomHash(const char* data, size_t n) {
   const uint32_t m = 0xc6a4a793u;
   uint32_t h = 0xbc9f1d34u ^ static_cast<uint32_t>(n * m);
   const unsigned char* p = reinterpret_cast<const unsigned char*>(data);
+  if (n == 20) {  // db_bench keys (key_size 20): five words, no tail
+    uint32_t w[5];
+    std::memcpy(w, p, 20);
+    for (int j = 0; j < 5; j++) {
+      h += w[j];
+      h *= m;
+      h ^= (h >> 16);
+    }
+    return h;
+  }
   size_t i = 0;
   for (; i + 4 <= n; i += 4) {
     uint32_t w;
@@ -151,6 +161,13 @@ class PinnedBytes {
     size_ += n;
     return true;
   }
+  // Room for n more bytes at the end (nullptr if it cannot grow); advance()
+  // then keeps any prefix of them -- AddKey's branch-free hash staging.
+  uint8_t* tail(size_t n) {
+    if (size_ + n > cap_ && !grow(size_ + n)) return nullptr;
+    return p_ + size_;
+  }
+  void advance(size_t n) { size_ += n; }
   void clear() { size_ = 0; }
   const uint8_t* data() const { return p_ ? p_ : reinterpret_cast<const uint8_t*>(""); }
   size_t size() const { return size_; }
@@ -221,14 +238,19 @@ class FullFilterBlockBuilder {
     if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
     if (opt_.hash_in_addkey) {
       const uint32_t h = BloomHash(key.data(), key.size());
-      if (n_ == 0 || h != last_hash_) {  // full_filter_block.cc:45-48
-        if (!keys_.append(reinterpret_cast<const char*>(&h), 4)) {
-          stage_status_ = DLSM_E_NOMEM;
-          return;
-        }
-        last_hash_ = h;
-        n_++;
+      uint8_t* t = keys_.tail(4);
+      if (!t) {
+        stage_status_ = DLSM_E_NOMEM;
+        return;
       }
+      // full_filter_block.cc:45-48, branch-free: the hash is always written
+      // and kept unless it repeats the previous one, so the next key's store
+      // address waits on one compare, not on this key's hash chain
+      std::memcpy(t, &h, 4);
+      const size_t keep = static_cast<size_t>((n_ == 0) | (h != last_hash_));
+      keys_.advance(4 * keep);
+      n_ += keep;
+      last_hash_ = h;
       return;
     }
     // the previous key is compared from a host copy: page-locked staging may
