@@ -101,6 +101,8 @@ def main():
                     help="1: capture one step (build + probe launches) in a HIP graph and replay it")
     ap.add_argument("--rehearse", action="store_true",
                     help="--gpus N in one process on a box with fewer GPUs: N logical devices on GPU 0")
+    ap.add_argument("--python-loop", action="store_true",
+                    help="N = 1: issue the timed steps from a Python loop instead of the native runner")
     ap.add_argument("--native", action="store_true",
                     help="time the steps with the library's native runner (dlsm_multi_device_run) at any N "
                          "(the default for --gpus N > 1; at N = 1 the Python loop is the default)")
@@ -204,7 +206,22 @@ def main():
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
 
-    for _ in range(args.warmup):
+    # The timed steps run from the library's native runner (a C++ loop issuing
+    # the same calls, dlsm_multi_device_run) unless an A/B knob needs the
+    # Python loop (HIP graph, co-scheduling, probe rounds, build groups) or
+    # --python-loop asks for it; the Python loop costs 3 % of the step on
+    # these boxes (profiles/r03_d_native_shares.txt vs r03_a_bench.json).
+    use_native = (world == 1 and not args.python_loop and not args.graph and not cosched
+                  and args.probe_round is None and not args.probe_serial and not args.build_groups)
+    if use_native:
+        from dlsm_amd import multigpu as MG
+
+        work, _keep = MG.device_work(ctx, ctx_b, inp)
+        elapsed, passes = MG.native_run([work], args.steps, args.warmup, bpk)
+        build_ms = float(np.mean([b for b, _ in passes]))
+        probe_ms = float(np.mean([p for _, p in passes]))
+        enqueue_s = float("nan")
+    for _ in range(0 if use_native else args.warmup):
         step()
     ctx.sync()
     ctx_b.sync()
@@ -218,17 +235,17 @@ def main():
         graph.replay()
         stream.synchronize()
 
-    # ---- timed region ----------------------------------------------------
+    # ---- timed region (Python loop) ---------------------------------------
     def ev():
         return torch.cuda.Event(enable_timing=True)
 
-    evs = [(ev(), ev(), ev(), ev()) for _ in range(args.steps)]
+    evs = [(ev(), ev(), ev(), ev()) for _ in range(0 if use_native else args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     pass_events = graph is None
-    for i in range(args.steps):
+    for i in range(0 if use_native else args.steps):
         if graph is not None:
             graph.replay()
             continue
@@ -249,17 +266,18 @@ def main():
             w = torch.cuda.Event()
             w.record(stream)
             stream_b.wait_event(w)
-    enqueue_s = time.perf_counter() - t0  # host time to submit the K steps
-    stream.synchronize()
-    stream_b.synchronize()
-    if part_stream is not None:
-        part_stream.synchronize()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = SH.max_over_ranks(elapsed, dist, dev)
-    if cosched or not pass_events:
+    if not use_native:
+        enqueue_s = time.perf_counter() - t0  # host time to submit the K steps
+        stream.synchronize()
+        stream_b.synchronize()
+        if part_stream is not None:
+            part_stream.synchronize()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        elapsed = SH.max_over_ranks(elapsed, dist, dev)
+    if not use_native and (cosched or not pass_events):
         # co-scheduled passes overlap, so the per-pass times (roofline) come
         # from the same K steps run one pass after another on one stream
         ctx.set_partition_stream(None)
@@ -271,8 +289,9 @@ def main():
             ctx.full_probe_dev(fs, qk, mask)
             evs[i][3].record(stream)
         stream.synchronize()
-    build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-    probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    if not use_native:
+        build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+        probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
 
     # keys of the whole job per step (every rank's share)
     rank_keys = len(tables) * N + qk.n
@@ -318,6 +337,7 @@ def main():
             "build_groups": args.build_groups,
             "overlap": overlap,
             "hip_graph": graph is not None,
+            "timed_by": "dlsm_multi_device_run (C++ loop)" if use_native else "Python loop",
             "cosched_build_slice_cus_per_xcd": cosched,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
@@ -326,7 +346,7 @@ def main():
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
         },
-        "host_enqueue_ms_per_step": round(enqueue_s / args.steps * 1e3, 4),
+        "host_enqueue_ms_per_step": None if use_native else round(enqueue_s / args.steps * 1e3, 4),
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
                   "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
         "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, qk.n) / probe_ms / 1e3, 1),

@@ -142,23 +142,8 @@ class DeviceWorker:
 
     def device_work(self):
         """This device's dlsm_device_work (the native runner's argument)."""
-        import ctypes as C
-
-        from . import _lib as L
-        from . import _ptr
-
-        inp = self.inp
-        caps = [int(o.numel()) for o in inp.outs]
-        jobs = self.ctx_b._jobs(inp.tables, inp.outs, caps)
-        w = L.dlsm_device_work()
-        w.probe_ctx, w.build_ctx = self.ctx.h.value, self.ctx_b.h.value
-        w.jobs = C.cast(jobs, C.c_void_p).value
-        w.n_jobs = len(inp.tables)
-        w.out_len_dev = _ptr(inp.lens)
-        w.fs = inp.fs.h.value if inp.lookups.n else None
-        w.keys = inp.lookups.c()
-        w.mask_dev = _ptr(inp.mask)
-        self._work_keep = (jobs, w)
+        w, keep = device_work(self.ctx, self.ctx_b, self.inp)
+        self._work_keep = keep
         return w
 
     def filter_digest(self) -> int:
@@ -253,22 +238,49 @@ def timed_run(workers, steps: int, warmup: int):
     return t1 - t0
 
 
-def native_timed_run(workers, steps: int, warmup: int, bits_per_key: int):
-    """The timed region run by the library's native runner
-    (dlsm_multi_device_run: a std::thread per device, host barriers on both
-    sides of the timed steps, device 0's passes timed with HIP events).
-    Returns (seconds, [(build_ms, probe_ms) per step] of device 0)."""
+def device_work(ctx, build_ctx, inp):
+    """dlsm_device_work for one device's inputs (sharding.RankInputs): the
+    build jobs on build_ctx, the probe on ctx.  Returns (struct, keep-alive)."""
+    import ctypes as C
+
+    from . import _lib as L
+    from . import _ptr
+
+    caps = [int(o.numel()) for o in inp.outs]
+    jobs = build_ctx._jobs(inp.tables, inp.outs, caps)
+    w = L.dlsm_device_work()
+    w.probe_ctx, w.build_ctx = ctx.h.value, build_ctx.h.value
+    w.jobs = C.cast(jobs, C.c_void_p).value
+    w.n_jobs = len(inp.tables)
+    w.out_len_dev = _ptr(inp.lens)
+    w.fs = inp.fs.h.value if inp.lookups.n else None
+    w.keys = inp.lookups.c()
+    w.mask_dev = _ptr(inp.mask)
+    return w, (jobs, w)
+
+
+def native_run(works, steps: int, warmup: int, bits_per_key: int):
+    """dlsm_multi_device_run over dlsm_device_work structs: (seconds,
+    [(build_ms, probe_ms) per step] of the first device)."""
     import ctypes as C
 
     from . import _lib as L
     from . import check, lib
 
-    arr = (L.dlsm_device_work * len(workers))(*[w.device_work() for w in workers])
+    arr = (L.dlsm_device_work * len(works))(*works)
     wall = C.c_double(0.0)
     pm = (C.c_float * (2 * steps))()
-    check(lib().dlsm_multi_device_run(arr, len(workers), bits_per_key, steps, warmup, C.byref(wall), pm),
+    check(lib().dlsm_multi_device_run(arr, len(works), bits_per_key, steps, warmup, C.byref(wall), pm),
           "multi_device_run")
     return wall.value, [(pm[2 * i], pm[2 * i + 1]) for i in range(steps)]
+
+
+def native_timed_run(workers, steps: int, warmup: int, bits_per_key: int):
+    """The timed region run by the library's native runner
+    (dlsm_multi_device_run: a std::thread per device, host barriers on both
+    sides of the timed steps, device 0's passes timed with HIP events).
+    Returns (seconds, [(build_ms, probe_ms) per step] of device 0)."""
+    return native_run([w.device_work() for w in workers], steps, warmup, bits_per_key)
 
 
 def build_workers(n_gpus: int, devices: list, T: int, N: int, Q: int, F: int, bpk: int,

@@ -134,6 +134,33 @@ inline uint32_t BloomHash(const char* data, size_t n) {
   return h;
 }
 
+// BloomHash of four 20-byte keys at p, p+20, p+40, p+60 (four independent
+// chains the CPU overlaps; same values as BloomHash).
+inline void BloomHash20x4(const char* p, uint32_t* out) {
+  const uint32_t m = 0xc6a4a793u;
+  uint32_t w[20];
+  std::memcpy(w, p, 80);
+  uint32_t h0 = 0xbc9f1d34u ^ static_cast<uint32_t>(20u * m), h1 = h0, h2 = h0, h3 = h0;
+  for (int j = 0; j < 5; j++) {
+    h0 += w[j];
+    h1 += w[5 + j];
+    h2 += w[10 + j];
+    h3 += w[15 + j];
+    h0 *= m;
+    h1 *= m;
+    h2 *= m;
+    h3 *= m;
+    h0 ^= h0 >> 16;
+    h1 ^= h1 >> 16;
+    h2 ^= h2 >> 16;
+    h3 ^= h3 >> 16;
+  }
+  out[0] = h0;
+  out[1] = h1;
+  out[2] = h2;
+  out[3] = h3;
+}
+
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
 struct FilterSlot {
   void* addr;
@@ -208,8 +235,9 @@ class PinnedBytes {
 //  * ctx only: its own context, one synchronous build per table;
 //  * batcher: the device's submission queue (dlsm_batcher): concurrent
 //    Finish calls of many builder threads become one batched build;
-//  * hash_in_addkey: AddKey computes BloomHash and drops a hash equal to
-//    the previous one on the host -- the reference's own AddKey
+//  * hash_in_addkey: AddKey's keys are hashed with BloomHash on the host
+//    (in blocks of 256: independent chains overlap) and a hash equal to the
+//    previous one is dropped -- the reference's own AddKey
 //    (full_filter_block.cc:39-49) -- so Finish moves 4 bytes per distinct
 //    key over PCIe instead of the key bytes, and the GPU builds from the
 //    hashes (dlsm_bloom_full_build_hashed).  Same filter bytes either way.
@@ -237,28 +265,23 @@ class FullFilterBlockBuilder {
   void AddKey(const Slice& key) {
     if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
     if (opt_.hash_in_addkey) {
-      const uint32_t h = BloomHash(key.data(), key.size());
-      uint8_t* t = keys_.tail(4);
-      if (!t) {
-        stage_status_ = DLSM_E_NOMEM;
-        return;
-      }
-      // full_filter_block.cc:45-48, branch-free: the hash is always written
-      // and kept unless it repeats the previous one, so the next key's store
-      // address waits on one compare, not on this key's hash chain
-      std::memcpy(t, &h, 4);
-      const size_t keep = static_cast<size_t>((n_ == 0) | (h != last_hash_));
-      keys_.advance(4 * keep);
-      n_ += keep;
-      last_hash_ = h;
+      // the key joins a small block of pending keys; every kHashBlock keys
+      // the block is hashed at once (independent hash chains overlap) and its
+      // hashes staged -- the same values, in the same order, as hashing in
+      // every AddKey call
+      if (pend_size_ + key.size() > pend_bytes_.size())
+        pend_bytes_.resize(2 * (pend_size_ + key.size()) + kHashBlock * 32);
+      std::memcpy(pend_bytes_.data() + pend_size_, key.data(), key.size());
+      pend_size_ += key.size();
+      pend_len_[pend_n_++] = static_cast<uint32_t>(key.size());
+      if (pend_n_ == kHashBlock) hash_pending();
       return;
     }
-    // the previous key is compared from a host copy: page-locked staging may
-    // be mapped uncached for the CPU, so it is written, never read back
+    const size_t prev0 = keys_.size() - last_len_;  // the previous key's offset
     if (n_ == 0) {
       key_len_ = key.size();
     } else {
-      if (key.size() == last_key_.size() && memcmp(last_key_.data(), key.data(), key.size()) == 0) dups_++;
+      if (key.size() == last_len_ && memcmp(keys_.data() + prev0, key.data(), last_len_) == 0) dups_++;
       if (uniform_ && key.size() != key_len_) {  // first key of another length: offsets from now on
         uniform_ = false;
         offsets_.resize(n_ + 1);
@@ -270,12 +293,13 @@ class FullFilterBlockBuilder {
       return;
     }
     if (!uniform_) offsets_.push_back(keys_.size());
-    last_key_.assign(key.data(), key.size());
+    last_len_ = key.size();
     n_++;
   }
   // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
   // buffer (the slot, or the buffer given to Move_buffer).
   void Finish() {
+    if (opt_.hash_in_addkey && pend_n_) hash_pending();
     if (stage_status_ != DLSM_OK) {
       status_ = stage_status_;
       result.Reset(result.data(), 0);
@@ -343,13 +367,48 @@ class FullFilterBlockBuilder {
   int status() const { return status_; }
 
  private:
+  // BloomHash of the pending keys into the staged hashes, dropping a hash
+  // equal to its predecessor (full_filter_block.cc:45-48) branch-free: every
+  // hash is written, the write position advances only for a kept one.
+  void hash_pending() {
+    uint8_t* t = keys_.tail(4 * pend_n_);
+    if (!t) {
+      stage_status_ = DLSM_E_NOMEM;
+      pend_size_ = pend_n_ = 0;
+      return;
+    }
+    uint32_t h[kHashBlock];
+    const char* p = pend_bytes_.data();
+    size_t i = 0;
+    // 20-byte keys four at a time: four independent multiply chains
+    for (; i + 4 <= pend_n_ && pend_len_[i] == 20 && pend_len_[i + 1] == 20 && pend_len_[i + 2] == 20 &&
+           pend_len_[i + 3] == 20;
+         i += 4, p += 80)
+      BloomHash20x4(p, h + i);
+    for (; i < pend_n_; i++) {
+      h[i] = BloomHash(p, pend_len_[i]);
+      p += pend_len_[i];
+    }
+    size_t kept = 0;
+    uint32_t last = last_hash_;
+    const bool first = n_ == 0;
+    for (size_t j = 0; j < pend_n_; j++) {
+      std::memcpy(t + 4 * kept, &h[j], 4);
+      kept += static_cast<size_t>((first && j == 0) | (h[j] != last));
+      last = h[j];
+    }
+    keys_.advance(4 * kept);
+    n_ += kept;
+    last_hash_ = last;
+    pend_size_ = pend_n_ = 0;
+  }
   void clear_keys() {
     keys_.clear();
     offsets_.clear();
     uniform_ = true;
-    key_len_ = 0;
-    last_key_.clear();
+    key_len_ = last_len_ = 0;
     n_ = dups_ = 0;
+    pend_size_ = pend_n_ = 0;
     stage_status_ = DLSM_OK;
   }
   FilterSlot* local_mr_;
@@ -361,8 +420,12 @@ class FullFilterBlockBuilder {
   uint32_t last_hash_ = 0;         // hash_in_addkey: the last staged hash
   std::vector<uint64_t> offsets_;  // key boundaries, only once lengths differ
   bool uniform_ = true;
-  size_t key_len_ = 0;
-  std::string last_key_;           // the previous key (AddKey's duplicate check)
+  size_t key_len_ = 0, last_len_ = 0;
+  // hash_in_addkey: keys pending hashing (bytes back to back + lengths)
+  static constexpr size_t kHashBlock = 256;
+  std::vector<char> pend_bytes_;  // capacity kept across tables
+  uint32_t pend_len_[kHashBlock];
+  size_t pend_size_ = 0, pend_n_ = 0;
   uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = 0;
   int status_ = DLSM_OK;        // the last Finish's result
