@@ -216,8 +216,8 @@ def main():
     if use_native:
         from dlsm_amd import multigpu as MG
 
-        work, _keep = MG.device_work(ctx, ctx_b, inp)
-        elapsed, passes = MG.native_run([work], args.steps, args.warmup, bpk)
+        dwork, _keep = MG.device_work(ctx, ctx_b, inp)
+        elapsed, passes = MG.native_run([dwork], args.steps, args.warmup, bpk)
         build_ms = float(np.mean([b for b, _ in passes]))
         probe_ms = float(np.mean([p for _, p in passes]))
         enqueue_s = float("nan")
