@@ -117,3 +117,18 @@ def test_bench_two_gpus_rehearsed():
     assert line["config"]["gpu_tables"] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
     assert line["config"]["gpu_lookups"] == [[0, 2_000_000], [2_000_000, 4_000_000]]
     assert line["value"] > 0 and line["roofline"]["achieved"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_one_gpu_native_and_python_loop():
+    """N = 1: the default times the steps with the native runner; --python-loop
+    the same calls from Python.  Both print a complete bench line."""
+    base = ["--steps", "3", "--warmup", "1", "--keys-per-table", "200000", "--lookups", "4000000",
+            "--no-cpu", "--no-e2e"]
+    for extra, timed_by in (([], "dlsm_multi_device_run"), (["--python-loop"], "Python loop")):
+        r = _bench(base + extra, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        assert line["n_gpus"] == 1 and line["config"]["timed_by"].startswith(timed_by)
+        assert line["value"] > 0 and line["probe"]["ms"] > 0 and line["build"]["ms"] > 0
+        assert line["roofline"]["hbm_read_GBs_measured"] > 1000
