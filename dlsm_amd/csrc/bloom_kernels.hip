@@ -552,7 +552,10 @@ __device__ __forceinline__ void seg_locate_set_lds(uint32_t excl, uint64_t nz, u
 // E: the walk's element -- uint32_t (one entry) or uint4 (a 16-byte unit of
 // four entries, for bucket offsets that are multiples of 4); CHUNK: a
 // chunk region's stride in elements.
-template <int U, uint32_t CHUNK, typename E = uint32_t>
+// NTL: the entry loads are non-temporal (the probe's 4 B/key entries are read
+// once; streaming them past the Infinity Cache keeps it for the answers the
+// unpermute pass reads next).
+template <int U, uint32_t CHUNK, typename E = uint32_t, bool NTL = false>
 struct SegWalk {
   static constexpr uint32_t kPerE = sizeof(E) / 4;  // entries per element
   const uint16_t* tb;
@@ -641,7 +644,14 @@ struct SegWalk {
   __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
     const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
 #pragma unroll
-    for (int u = 0; u < U; u++) hv[u] = gent[idx[u]];  // in-group for every lane: no select around the load
+    for (int u = 0; u < U; u++) {  // in-group for every lane: no select around the load
+      if constexpr (NTL && sizeof(E) == 16) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(gent + idx[u]));
+        hv[u] = make_uint4(x.x, x.y, x.z, x.w);
+      } else {
+        hv[u] = gent[idx[u]];
+      }
+    }
   }
 };
 
@@ -655,12 +665,12 @@ struct WinSet {
   bool ok[U];
 };
 
-template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, typename Act>
+template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL = false, typename Act>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
                                               uint32_t* scratch, Act act) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
-  SegWalk<U, CHUNK, E> w{tb, entries, rowlen, g_step, g_end, gs};
+  SegWalk<U, CHUNK, E, NTL> w{tb, entries, rowlen, g_step, g_end, gs};
   w.scr = (lds_u32*)scratch;  // generic -> LDS address space (addrspacecast)
   if (!w.start(g_first)) return;
   WinSet<U, CHUNK, E> A, B;
@@ -881,6 +891,9 @@ constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
 constexpr int kWalkU = DLSM_BUILD_WALKU;  // hashes in flight per lane (build segment walk)
 #ifndef DLSM_PROBE_U
 #define DLSM_PROBE_U 1
+#endif
+#ifndef DLSM_PROBE_NTL
+#define DLSM_PROBE_NTL 1  // non-temporal entry loads in the probe slice pass
 #endif
 #ifndef DLSM_PROBE_DEPTH
 #define DLSM_PROBE_DEPTH 1  // window sets of loads in flight per wave (walk_segments)
@@ -1369,7 +1382,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
   const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
-  walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH>(
+  walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
       tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch,
       [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
@@ -1429,6 +1442,17 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
       });
 }
 
+// Eight positions (16 bytes) of the unpermute: read once, non-temporal with
+// DLSM_PROBE_NTL (see SegWalk).
+__device__ __forceinline__ uint4 load_pos8(const uint16_t* p) {
+#if DLSM_PROBE_NTL
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
 // Pass 3: one workgroup per chunk: stage the chunk's bucketed answers in LDS
 // (16-byte loads), gather them back to key order through pos (16-byte loads
 // of 8 positions), store 8 answers per lane.
@@ -1452,7 +1476,7 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
   __syncthreads();
   for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
     if (i0 + 8u <= nk) {
-      const uint4 pv = *reinterpret_cast<const uint4*>(pos + first + i0);
+      const uint4 pv = load_pos8(pos + first + i0);
       const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
       uint32_t lo = 0, hi = 0;
 #pragma unroll
@@ -2023,7 +2047,7 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_group_kernel(
   // accesses at the group's byte of each key's stride.
   for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
     if (i0 + 8u <= nk) {
-      const uint4 pv = *reinterpret_cast<const uint4*>(pos + first + i0);
+      const uint4 pv = load_pos8(pos + first + i0);
       const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
       uint32_t lo = 0, hi = 0;
 #pragma unroll

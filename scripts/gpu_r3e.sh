@@ -8,6 +8,11 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || exit 2
 timeout -k 10 200 python bench.py --python-loop --no-cpu --no-e2e > "$OUT/bench_pyloop.json" 2> "$OUT/bench_pyloop.err" || exit 2
+for r in 1 2 3; do
+  timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu --no-e2e > "$OUT/ntl1_r$r.json" 2> "$OUT/ntl1_r$r.err" || exit 2
+  DLSM_LIB_VARIANT=ntl0 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu --no-e2e \
+    > "$OUT/ntl0_r$r.json" 2> "$OUT/ntl0_r$r.err" || exit 2
+done
 run() {  # name "ENV=.." extra-bench-args...
   local name=$1 envs=$2; shift 2
   env $envs timeout -k 10 120 python bench.py --native --steps 100 --warmup 10 $SHARE "$@" \
