@@ -33,6 +33,9 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 #include <string>
 #include <vector>
 
@@ -161,6 +164,44 @@ inline void BloomHash20x4(const char* p, uint32_t* out) {
   out[3] = h3;
 }
 
+#if defined(__x86_64__) && (defined(__GNUC__) || defined(__clang__))
+// BloomHash of sixteen 20-byte keys at p .. p+300 with AVX-512: the 80 words
+// load as five 16-lane vectors, word j of key k (dword 5k + j) is gathered
+// across them with two-source permutes, and the five hash rounds run on all
+// 16 keys at once.  Same values as BloomHash; used when the CPU has AVX-512F
+// (dlsm_adapter::HasAvx512).
+__attribute__((target("avx512f"))) inline void BloomHash20x16(const char* p, uint32_t* out) {
+  const __m512i v0 = _mm512_loadu_si512(p), v1 = _mm512_loadu_si512(p + 64), v2 = _mm512_loadu_si512(p + 128),
+                v3 = _mm512_loadu_si512(p + 192), v4 = _mm512_loadu_si512(p + 256);
+  const __m512i k = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  const __m512i k5 = _mm512_mullo_epi32(k, _mm512_set1_epi32(5));
+  const __m512i m = _mm512_set1_epi32(static_cast<int>(0xc6a4a793u));
+  __m512i h = _mm512_set1_epi32(static_cast<int>(0xbc9f1d34u ^ (20u * 0xc6a4a793u)));
+  for (int j = 0; j < 5; j++) {
+    const __m512i d = _mm512_add_epi32(k5, _mm512_set1_epi32(j));  // dword index 5k + j, 0..79
+    const __m512i lo = _mm512_permutex2var_epi32(v0, d, v1);          // d in [0, 32)
+    const __m512i mid = _mm512_permutex2var_epi32(v2, d, v3);         // d in [32, 64)
+    const __m512i hi = _mm512_permutexvar_epi32(d, v4);               // d in [64, 80)
+    const __mmask16 ge32 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(32));
+    const __mmask16 ge64 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(64));
+    const __m512i w = _mm512_mask_blend_epi32(ge64, _mm512_mask_blend_epi32(ge32, lo, mid), hi);
+    h = _mm512_add_epi32(h, w);
+    h = _mm512_mullo_epi32(h, m);
+    h = _mm512_xor_si512(h, _mm512_srli_epi32(h, 16));
+  }
+  _mm512_storeu_si512(out, h);
+}
+inline bool HasAvx512() {
+  static const bool has = __builtin_cpu_supports("avx512f");
+  return has;
+}
+#else
+inline void BloomHash20x16(const char* p, uint32_t* out) {
+  for (int q = 0; q < 4; q++) BloomHash20x4(p + 80 * q, out + 4 * q);
+}
+inline bool HasAvx512() { return false; }
+#endif
+
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
 struct FilterSlot {
   void* addr;
@@ -273,6 +314,7 @@ class FullFilterBlockBuilder {
         pend_bytes_.resize(2 * (pend_size_ + key.size()) + kHashBlock * 32);
       std::memcpy(pend_bytes_.data() + pend_size_, key.data(), key.size());
       pend_size_ += key.size();
+      pend_fixed20_ = pend_fixed20_ && key.size() == 20;
       pend_len_[pend_n_++] = static_cast<uint32_t>(key.size());
       if (pend_n_ == kHashBlock) hash_pending();
       return;
@@ -375,12 +417,16 @@ class FullFilterBlockBuilder {
     if (!t) {
       stage_status_ = DLSM_E_NOMEM;
       pend_size_ = pend_n_ = 0;
+      pend_fixed20_ = true;
       return;
     }
     uint32_t h[kHashBlock];
     const char* p = pend_bytes_.data();
     size_t i = 0;
-    // 20-byte keys four at a time: four independent multiply chains
+    // 20-byte keys 16 at a time (AVX-512) or four at a time (four
+    // independent multiply chains)
+    if (pend_fixed20_ && HasAvx512())
+      for (; i + 16 <= pend_n_; i += 16, p += 320) BloomHash20x16(p, h + i);
     for (; i + 4 <= pend_n_ && pend_len_[i] == 20 && pend_len_[i + 1] == 20 && pend_len_[i + 2] == 20 &&
            pend_len_[i + 3] == 20;
          i += 4, p += 80)
@@ -401,6 +447,7 @@ class FullFilterBlockBuilder {
     n_ += kept;
     last_hash_ = last;
     pend_size_ = pend_n_ = 0;
+    pend_fixed20_ = true;
   }
   void clear_keys() {
     keys_.clear();
@@ -409,6 +456,7 @@ class FullFilterBlockBuilder {
     key_len_ = last_len_ = 0;
     n_ = dups_ = 0;
     pend_size_ = pend_n_ = 0;
+    pend_fixed20_ = true;
     stage_status_ = DLSM_OK;
   }
   FilterSlot* local_mr_;
@@ -426,6 +474,7 @@ class FullFilterBlockBuilder {
   std::vector<char> pend_bytes_;  // capacity kept across tables
   uint32_t pend_len_[kHashBlock];
   size_t pend_size_ = 0, pend_n_ = 0;
+  bool pend_fixed20_ = true;  // every pending key is 20 bytes
   uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = 0;
   int status_ = DLSM_OK;        // the last Finish's result

@@ -43,6 +43,19 @@ int main() {
         CHECK(dlsm_adapter::BloomHash(k.data(), n) == dlsm_bloom_hash(k.data(), n));
     }
     CHECK(dlsm_adapter::BloomHash("\xc3\x97", 2) == 0x0f2ba540u);  // the reference code's value
+    // the 4- and 16-key block forms AddKey uses for 20-byte keys
+    std::vector<char> b(320 * 50);
+    for (auto& c : b) {
+      x = x * 1664525u + 1013904223u;
+      c = static_cast<char>(x >> 24);
+    }
+    for (size_t o = 0; o + 320 <= b.size(); o += 320) {
+      uint32_t h4[4], h16[16];
+      dlsm_adapter::BloomHash20x4(b.data() + o, h4);
+      dlsm_adapter::BloomHash20x16(b.data() + o, h16);
+      for (int i = 0; i < 16; i++) CHECK(h16[i] == dlsm_bloom_hash(b.data() + o + 20 * i, 20));
+      for (int i = 0; i < 4; i++) CHECK(h4[i] == h16[i]);
+    }
   }
   // the staging-buffer claim needs a context
   CHECK(dlsm_ctx_host_buffer_claim(nullptr, &b) == DLSM_E_ARG);
