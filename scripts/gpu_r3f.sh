@@ -16,3 +16,13 @@ for SHARE in "--tables 16 --lookups 100000000" "--tables 2 --lookups 12500000" "
     done
   done
 done
+g++ -std=c++17 -O2 -fno-rtti -fno-exceptions -pthread -I include tests/cpp/concurrent_builders.cc \
+  -L dlsm_amd/lib -ldlsm_bloom -L oracle -loracle -Wl,-rpath,$PWD/dlsm_amd/lib -Wl,-rpath,$PWD/oracle \
+  -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -o "$OUT/cb" || exit 3
+for r in 1 2; do
+  for mode in hash ctx; do
+    for t in 1 4 8 16; do
+      timeout -k 10 200 "$OUT/cb" $t 8 153846 $mode >> "$OUT/concurrent_builders.jsonl" 2>> "$OUT/cb.err" || exit 4
+    done
+  done
+done
