@@ -35,6 +35,7 @@ INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbforma
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
+OPT_SMALL_BUILD = 7
 
 
 def lib():
@@ -283,6 +284,15 @@ class Context:
     def set_build_exact(self, mode: int):
         """0 auto, 1 count distinct hashes before bucketing, 2 never (DLSM_OPT_BUILD_EXACT)."""
         self.set_option(OPT_BUILD_EXACT, mode)
+
+    def set_small_build(self, on: bool):
+        """Small hashed build jobs in one launch (DLSM_OPT_SMALL_BUILD, default off)."""
+        self.set_option(OPT_SMALL_BUILD, 1 if on else 0)
+
+    def get_option(self, option: int) -> int:
+        v = C.c_uint64()
+        check(lib().dlsm_ctx_get_option(self.h, option, C.byref(v)), "get_option")
+        return int(v.value)
 
     def set_probe_shape(self, chunk_lg: int, slice_lg: int):
         """Sliced probe shape: 2^chunk_lg keys per partition chunk (12..14),

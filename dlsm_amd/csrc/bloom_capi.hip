@@ -107,6 +107,7 @@ struct dlsm_ctx {
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
+  bool small_build = false;   // DLSM_OPT_SMALL_BUILD: small hashed jobs in one launch
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -397,6 +398,7 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SERIAL")) ctx->probe_serial = atoi(v) != 0;
+  if (const char* v = getenv("DLSM_SMALL_BUILD")) ctx->small_build = atoi(v) != 0;
   *out = ctx;
   return DLSM_OK;
 }
@@ -519,6 +521,10 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > 1) return DLSM_E_ARG;
       ctx->probe_serial = value != 0;
       return DLSM_OK;
+    case DLSM_OPT_SMALL_BUILD:
+      if (value > 1) return DLSM_E_ARG;
+      ctx->small_build = value != 0;
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -534,6 +540,7 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_PROBE_SLICE_LG: *value = static_cast<uint64_t>(ctx->probe_lgr); return DLSM_OK;
     case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
     case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
+    case DLSM_OPT_SMALL_BUILD: *value = ctx->small_build ? 1u : 0u; return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -748,6 +755,10 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
   // the slice pass's fallback for a lowered line count is not available.
   const bool exact = sliced_ok && (hashed || ctx->build_exact == 1 ||
                                    (ctx->build_exact == 0 && (any_suffix || mode == KM_GENERIC)));
+  // Small hashed jobs (one builder thread's Finish) build in one launch: job j
+  // gets ceil(L / kSmallLines) workgroups (full_small_hashed_kernel).
+  bool small = hashed && ctx->path == 0 && ctx->small_build;
+  for (int j = 0; j < n_jobs && small; j++) small = Ls[j] <= kSmallMaxWGs * kSmallLines;
 
   std::vector<FullJobDev> hj(n_jobs);
   std::vector<uint32_t> starts(2 * n_jobs);
@@ -765,7 +776,9 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
     d.chunk0 = chunk;
     d.L_spec = Ls[j];
     d.magic_spec = Ls[j] ? fastmod_magic(Ls[j]) : 0;
-    d.n_slices = sliced_ok ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], 1ull << lgR)) : 1;
+    d.n_slices = small       ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], kSmallLines))
+                 : sliced_ok ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], 1ull << lgR))
+                             : 1;
     d.slice0 = slice;
     d.tab0 = tabw;
     d.k = k;
@@ -797,6 +810,10 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
     ctx->last_starts = starts;
     ctx->last_jobs_gen = ctx->jobs.gen;
     ctx->last_starts_gen = ctx->starts.gen;
+  }
+  if (small) {
+    DLSM_TRY(launch_full_small_hashed(ctx->jobs.p, ctx->starts.p + n_jobs, n_jobs, slice, s));
+    return DLSM_OK;
   }
   DLSM_CHECK(ctx->dchunk.ensure(chunk));
   DLSM_CHECK(ctx->jobL.ensure(n_jobs));

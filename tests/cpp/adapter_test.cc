@@ -255,6 +255,57 @@ int main() {
             (orc_filter_block_key_may_match(want.data(), wl, key_block[i],
                                             reinterpret_cast<const uint8_t*>(ks[i].data()), 20, 0) != 0));
   }
+  // ---- hash_in_addkey: AddKey hashes on the host (block / AVX-512 forms),
+  // Finish sends the hashes; variable-length keys with sign-extended tails,
+  // runs of repeated keys, and 20-byte runs that straddle hash blocks; alone,
+  // through a batcher, and with the hashes from 20-byte keys only ----
+  {
+    dlsm_batcher* bat = nullptr;
+    CHECK(dlsm_batcher_create(0, 2, 0, 16, &bat) == DLSM_OK);
+    for (int shape = 0; shape < 3; shape++) {
+      for (int via_batcher = 0; via_batcher < 2; via_batcher++) {
+        std::vector<char> slot(1 << 20, 0);
+        dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+        dlsm_adapter::BuilderOptions opt;
+        opt.hash_in_addkey = true;
+        if (via_batcher) opt.batcher = bat;
+        dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx, opt);
+        std::string flat;
+        std::vector<uint64_t> offs{0};
+        uint32_t x = 777u + shape;
+        const int n = shape == 0 ? 70001 : 9000;
+        for (int i = 0; i < n; i++) {
+          std::string k;
+          if (shape == 0 || (shape == 2 && i % 300 < 250)) {  // 20-byte db_bench keys
+            uint8_t kk[20];
+            orc_dbbench_key(static_cast<uint64_t>(i), 20, kk);
+            k.assign(reinterpret_cast<char*>(kk), 20);
+          } else {  // 0..33 random bytes (>= 0x80 included: sign-extended tails)
+            x = x * 1664525u + 1013904223u;
+            const int len = static_cast<int>(x >> 27);
+            for (int j = 0; j < len; j++) {
+              x = x * 1664525u + 1013904223u;
+              k.push_back(static_cast<char>(x >> 24));
+            }
+          }
+          const int reps = (i % 11 == 0) ? 3 : 1;  // consecutive duplicates
+          for (int r = 0; r < reps; r++) {
+            b.AddKey(Slice(k));
+            flat += k;
+            offs.push_back(flat.size());
+          }
+        }
+        b.Finish();
+        CHECK(b.status() == DLSM_OK);
+        std::vector<uint8_t> want(1 << 20, 0);
+        const int64_t wl = orc_full_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0,
+                                          offs.size() - 1, 10, want.data(), want.size());
+        CHECK(wl > 0 && static_cast<int64_t>(b.result.size()) == wl);
+        CHECK(std::memcmp(b.result.data(), want.data(), wl) == 0);
+      }
+    }
+    dlsm_batcher_destroy(bat);
+  }
   // ---- two live builders on ONE context: the second stages into a
   // private pinned buffer, both filters stay exact ----
   {

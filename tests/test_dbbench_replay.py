@@ -74,6 +74,7 @@ def test_replay_parity_with_compactions(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(600)  # ~150 s of work; outlasts a suite-wide --timeout 120
 def test_replay_config5_full_size(gpu):
     """BASELINE config 5 at its stated size: db_bench --num=6250000 x 16
     threads = 100 M fillrandom writes (651 flushes + leveled compactions, every
