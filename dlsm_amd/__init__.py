@@ -35,7 +35,6 @@ INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbforma
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
-OPT_SMALL_BUILD = 7
 
 
 def lib():
@@ -55,6 +54,22 @@ def bloom_hash(key: bytes) -> int:
     """BloomHash (include/TimberSaw/filter_policy.h:26-28), host side."""
     b = C.create_string_buffer(bytes(key), len(key) + 1)
     return int(lib().dlsm_bloom_hash(b, len(key)))
+
+
+class PinnedArray:
+    """A page-locked host uint8 array (dlsm_host_alloc), freed on close()."""
+
+    def __init__(self, nbytes: int):
+        p = C.c_void_p()
+        check(lib().dlsm_host_alloc(nbytes, C.byref(p)), "host_alloc")
+        self.ptr = p.value
+        self.array = np.ctypeslib.as_array((C.c_uint8 * nbytes).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            lib().dlsm_host_free(C.c_void_p(self.ptr))
+            self.ptr = None
+            self.array = None
 
 
 def full_size(n_dedup: int, bits_per_key: int = 10):
@@ -284,10 +299,6 @@ class Context:
     def set_build_exact(self, mode: int):
         """0 auto, 1 count distinct hashes before bucketing, 2 never (DLSM_OPT_BUILD_EXACT)."""
         self.set_option(OPT_BUILD_EXACT, mode)
-
-    def set_small_build(self, on: bool):
-        """Small hashed build jobs in one launch (DLSM_OPT_SMALL_BUILD, default off)."""
-        self.set_option(OPT_SMALL_BUILD, 1 if on else 0)
 
     def get_option(self, option: int) -> int:
         v = C.c_uint64()

@@ -107,7 +107,6 @@ struct dlsm_ctx {
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
-  bool small_build = false;   // DLSM_OPT_SMALL_BUILD: small hashed jobs in one launch
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -142,6 +141,12 @@ struct dlsm_ctx {
   DevBuf<uint32_t> crc_val;
   // internal-key selection / gather: [blk_cnt | blk_bytes | tot(2) | first_bad]
   DevBuf<uint64_t> sel;
+  // host-API results: page-locked, device-mapped, so the build kernels store
+  // filters and lengths straight to host memory (one synchronisation, no D2H)
+  uint8_t* h_out = nullptr;
+  uint64_t h_out_cap = 0;
+  uint64_t* h_len = nullptr;
+  uint64_t h_len_cap = 0;
   // page-locked host staging lent to the context's (single) builder
   void* host_buf = nullptr;
   uint64_t host_cap = 0;
@@ -398,7 +403,6 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SERIAL")) ctx->probe_serial = atoi(v) != 0;
-  if (const char* v = getenv("DLSM_SMALL_BUILD")) ctx->small_build = atoi(v) != 0;
   *out = ctx;
   return DLSM_OK;
 }
@@ -441,6 +445,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
+  if (ctx->h_out) (void)hipHostFree(ctx->h_out);
+  if (ctx->h_len) (void)hipHostFree(ctx->h_len);
   delete ctx;
   return DLSM_OK;
 }
@@ -521,10 +527,6 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > 1) return DLSM_E_ARG;
       ctx->probe_serial = value != 0;
       return DLSM_OK;
-    case DLSM_OPT_SMALL_BUILD:
-      if (value > 1) return DLSM_E_ARG;
-      ctx->small_build = value != 0;
-      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -540,7 +542,6 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_PROBE_SLICE_LG: *value = static_cast<uint64_t>(ctx->probe_lgr); return DLSM_OK;
     case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
     case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
-    case DLSM_OPT_SMALL_BUILD: *value = ctx->small_build ? 1u : 0u; return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -755,10 +756,6 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
   // the slice pass's fallback for a lowered line count is not available.
   const bool exact = sliced_ok && (hashed || ctx->build_exact == 1 ||
                                    (ctx->build_exact == 0 && (any_suffix || mode == KM_GENERIC)));
-  // Small hashed jobs (one builder thread's Finish) build in one launch: job j
-  // gets ceil(L / kSmallLines) workgroups (full_small_hashed_kernel).
-  bool small = hashed && ctx->path == 0 && ctx->small_build;
-  for (int j = 0; j < n_jobs && small; j++) small = Ls[j] <= kSmallMaxWGs * kSmallLines;
 
   std::vector<FullJobDev> hj(n_jobs);
   std::vector<uint32_t> starts(2 * n_jobs);
@@ -776,9 +773,7 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
     d.chunk0 = chunk;
     d.L_spec = Ls[j];
     d.magic_spec = Ls[j] ? fastmod_magic(Ls[j]) : 0;
-    d.n_slices = small       ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], kSmallLines))
-                 : sliced_ok ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], 1ull << lgR))
-                             : 1;
+    d.n_slices = sliced_ok ? std::max<uint32_t>(1, ceil_div_u32(Ls[j], 1ull << lgR)) : 1;
     d.slice0 = slice;
     d.tab0 = tabw;
     d.k = k;
@@ -810,10 +805,6 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
     ctx->last_starts = starts;
     ctx->last_jobs_gen = ctx->jobs.gen;
     ctx->last_starts_gen = ctx->starts.gen;
-  }
-  if (small) {
-    DLSM_TRY(launch_full_small_hashed(ctx->jobs.p, ctx->starts.p + n_jobs, n_jobs, slice, s));
-    return DLSM_OK;
   }
   DLSM_CHECK(ctx->dchunk.ensure(chunk));
   DLSM_CHECK(ctx->jobL.ensure(n_jobs));
@@ -914,6 +905,38 @@ int stage_keys(dlsm_ctx* ctx, const dlsm_keyset* const* sets, int n, std::vector
 }  // namespace
 
 namespace {
+// Grow a page-locked host array (contents dropped; the context stream is idle
+// between host-API calls, so no queued command still uses the old one).
+extern "C++" template <typename T>
+int host_ensure(T*& p, uint64_t& cap, uint64_t n) {
+  if (n <= cap && p) return DLSM_OK;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  const uint64_t want = std::max<uint64_t>(n, 64);
+  DLSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&p), want * sizeof(T), hipHostMallocDefault));
+  cap = want;
+  return DLSM_OK;
+}
+
+// The device address of a page-locked host pointer (hipHostMalloc'd, or
+// registered: dlsm_host_register), or nullptr for pageable memory.
+uint8_t* host_device_view(void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // not HIP memory: clear the error the query left
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  const uintptr_t off = a.hostPointer ? reinterpret_cast<uintptr_t>(p) - reinterpret_cast<uintptr_t>(a.hostPointer) : 0;
+  return static_cast<uint8_t*>(a.devicePointer) + off;
+}
+
+// Host keys -> host filters.  The keys go H2D into the context's staging; the
+// build kernels write each filter straight into the caller's slot when it is
+// page-locked (16-byte aligned), else into page-locked staging copied out
+// afterwards, and the lengths into page-locked memory: one stream
+// synchronisation per call and no device-to-host copy commands.
 int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
                          uint64_t* out_len, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
@@ -928,32 +951,36 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
   std::vector<dlsm_keyset> dk;
   DLSM_CHECK(stage_keys(ctx, sets.data(), n_jobs, dk));
   std::vector<dlsm_build_job> dj(n_jobs);
+  std::vector<uint8_t*> direct(n_jobs);
   uint64_t obytes = 0;
   std::vector<uint64_t> opos(n_jobs);
   for (int j = 0; j < n_jobs; j++) {
     const uint64_t spec = full_filter_len(jobs[j].keys.n, bits_per_key);
     const uint64_t cap = std::min(spec, jobs[j].out_cap);
+    direct[j] = host_device_view(jobs[j].out);
+    if (direct[j] && !aligned(direct[j], 16)) direct[j] = nullptr;
     opos[j] = obytes;
-    obytes += (cap + 255) & ~uint64_t(255);
+    if (!direct[j]) obytes += (cap + 255) & ~uint64_t(255);
     dj[j].keys = dk[j];
     dj[j].out_cap = cap;
   }
-  DLSM_CHECK(ctx->st_out.ensure(obytes + 256));
-  DLSM_CHECK(ctx->st_len.ensure(n_jobs));
-  for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
-  DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p, hashed));
-  hipStream_t s = ctx->stream;
-  DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_CHECK(host_ensure(ctx->h_out, ctx->h_out_cap, obytes + 256));
+  DLSM_CHECK(host_ensure(ctx->h_len, ctx->h_len_cap, static_cast<uint64_t>(n_jobs)));
+  uint8_t* h_out_dev = host_device_view(ctx->h_out);
+  uint64_t* h_len_dev = reinterpret_cast<uint64_t*>(host_device_view(ctx->h_len));
+  if (!h_out_dev || !h_len_dev) return DLSM_E_DEVICE;
+  for (int j = 0; j < n_jobs; j++) dj[j].out = direct[j] ? direct[j] : h_out_dev + opos[j];
+  DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, h_len_dev, hashed));
+  DLSM_TRY(hipStreamSynchronize(ctx->stream));
   int st = DLSM_OK;
   for (int j = 0; j < n_jobs; j++) {
+    out_len[j] = ctx->h_len[j];
     if (out_len[j] == 0) {
       st = DLSM_E_CAPACITY;
       continue;
     }
-    DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
+    if (!direct[j]) memcpy(jobs[j].out, ctx->h_out + opos[j], out_len[j]);
   }
-  DLSM_TRY(hipStreamSynchronize(s));
   return st;
 }
 }  // namespace

@@ -100,13 +100,6 @@ constexpr int kBuildChunk = DLSM_BUILD_CHUNK;  // keys per partition chunk (buil
 // plus up to 3 pads per bucket).  r02: build slice 65.7 -> 50.8 us
 // (profiles/r02_ab_units_pred.txt).
 constexpr uint32_t kBuildRegion = kBuildChunk + 4u * kMaxSlices;
-// One-pass build of small hashed jobs (full_small_hashed_kernel): lines per
-// workgroup (64 KiB of LDS), workgroup size, and the largest job it takes --
-// every workgroup reads all of its job's hashes, so only jobs of a few
-// workgroups go there.
-constexpr uint32_t kSmallLines = 1024;
-constexpr int kSmallBlock = 1024;
-constexpr uint32_t kSmallMaxWGs = 4;
 constexpr int kProbeChunkMin = 4096;  // smallest probe partition chunk (lgC 12)
 // u32 entries (and answer bytes) per probe chunk region: C keys plus up to 3
 // padding entries per slice bucket (buckets are padded to 16-byte units).
@@ -132,10 +125,6 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
                               const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s);
-// Small hashed jobs in one pass: job j runs n_slices workgroups from wg0s[j]
-// (slice0), each owning <= kSmallLines lines of the filter.
-hipError_t launch_full_small_hashed(const FullJobDev* jobs, const uint32_t* wg0s, int n_jobs,
-                                    uint32_t total_wgs, hipStream_t s);
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
                                int mode, hipStream_t s);

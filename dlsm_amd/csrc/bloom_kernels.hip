@@ -1056,105 +1056,6 @@ __global__ __launch_bounds__(kBlock) void full_scatter_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Full filter build, one pass for small hashed tables (the Finish of one
-// builder thread: ~150 K BloomHash values, a ~190 KB filter).  The job's W =
-// n_slices workgroups each own a range of <= kSmallLines lines in LDS and read
-// ALL of the job's hashes (4 B each, L2-resident after the first read) twice:
-// once to count the distinct ones (AddKey's consecutive-hash dedup,
-// full_filter_block.cc:39-49) -> the true line count, once to OR the hashes of
-// their range in.  One launch instead of count + partition + slice: for a
-// table this small the launches and their gaps, not the bytes, are the cost.
-// ---------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(NT) void full_small_hashed_kernel(const FullJobDev* __restrict__ jobs,
-                                                               const uint32_t* __restrict__ wg0s, int n_jobs) {
-  constexpr int U = 8;  // 16-byte loads (4 hashes) in flight per thread
-  __shared__ __attribute__((aligned(16))) uint32_t sl[kSmallLines * 16];
-  __shared__ uint32_t wsum[NT / 64];
-  __shared__ int sj;
-  const int tid = threadIdx.x, lane = tid & 63;
-  if (tid == 0) sj = find_job(wg0s, n_jobs, static_cast<uint32_t>(blockIdx.x));
-  for (uint32_t w = tid; w < kSmallLines * 16; w += NT) sl[w] = 0;
-  __syncthreads();
-  const FullJobDev J = jobs[sj];
-  const uint32_t wg = blockIdx.x - J.slice0, W = J.n_slices;
-  const uint32_t* hs = reinterpret_cast<const uint32_t*>(J.keys.bytes);
-  const int n = static_cast<int>(J.keys.n);
-  // The hashes as 16-byte vectors from the 16-byte boundary at or below hs
-  // (the hashes are 4-byte aligned; the o < 4 words before hs and the words
-  // past the end share 16-byte blocks, so pages, with real hashes): vector q
-  // holds hashes 4q - o .. 4q - o + 3.  Lane l's vectors follow lane l-1's, so
-  // a vector's predecessor hash is lane l-1's last word; lane 0 loads its own.
-  const uint4* hv = reinterpret_cast<const uint4*>(reinterpret_cast<uintptr_t>(hs) & ~uintptr_t(15));
-  const int o = static_cast<int>((reinterpret_cast<uintptr_t>(hs) & 15u) >> 2);
-  const int nv = (n + o + 3) / 4;
-  auto sweep = [&](auto&& f) {
-    for (int b = 0; b < nv; b += NT * U) {
-      uint4 v[U];
-      uint32_t p0[U];
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int q = b + u * NT + tid;
-        v[u] = q < nv ? hv[q] : make_uint4(0, 0, 0, 0);
-        const int e = 4 * q - o;  // hash index of v[u].x
-        p0[u] = (lane == 0 && q < nv && e >= 1) ? hs[e - 1] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int e = 4 * (b + u * NT + tid) - o;
-        const uint32_t up = __shfl_up(v[u].w, 1, 64);
-        uint32_t prev = lane == 0 ? p0[u] : up;
-        const uint32_t h4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          // AddKey's check: the first hash, or one unequal to its predecessor
-          f(h4[c], e + c >= 0 && e + c < n && (e + c == 0 || h4[c] != prev));
-          prev = h4[c];
-        }
-      }
-    }
-  };
-  uint32_t cnt = 0;
-  sweep([&](uint32_t, bool keep) { cnt += keep ? 1u : 0u; });
-  const uint32_t ws = wave_sum(cnt);
-  if (lane == 0) wsum[tid >> 6] = ws;
-  __syncthreads();
-  uint32_t distinct = 0;
-#pragma unroll
-  for (int q = 0; q < NT / 64; q++) distinct += wsum[q];
-  uint32_t total_bits;
-  const uint32_t L = full_num_lines(distinct, J.bpk, &total_bits);
-  const uint64_t len = static_cast<uint64_t>(total_bits / 8u) + 5u;
-  if (len > J.out_cap) {
-    if (wg == 0 && tid == 0) *J.out_len = 0;
-    return;
-  }
-  // L <= L_spec <= W * kSmallLines (the host sized W from the n-hash count)
-  const uint32_t RW = (L + W - 1u) / W;
-  const uint32_t lo = wg * RW;
-  const uint32_t nl = lo < L ? min(RW, L - lo) : 0u;
-  if (nl > 0) {
-    const uint32_t magic = fastmod_magic(L);
-    const int k = J.k;
-    sweep([&](uint32_t h, bool keep) {
-      const uint32_t off = fastmod(h, L, magic) - lo;  // wraps for lines below the range
-      if (keep && off < nl) {
-        if (k == 6) lds_add_hash_k<6>(sl + off * 16u, h);
-        else lds_add_hash(sl + off * 16u, h, k);
-      }
-    });
-    __syncthreads();
-    uint4* dst = reinterpret_cast<uint4*>(J.out + static_cast<uint64_t>(lo) * 64u);
-    const uint4* src = reinterpret_cast<const uint4*>(sl);
-    for (uint32_t w = tid; w < nl * 4u; w += NT) dst[w] = src[w];
-  }
-  if (wg == 0 && tid == 0) {
-    write_trailer(J.out, L, J.k);
-    *J.out_len = len;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Full filter probe, direct: one thread per key, global reads of the filters.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t full_may_match(uint32_t h, const FilterDev& f) {
@@ -1818,13 +1719,6 @@ hipError_t launch_full_scatter(const FullJobDev* jobs, const uint32_t* chunk0s, 
     full_scatter_kernel<KM_HASH><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
   else
     full_scatter_kernel<KM_GENERIC><<<total_chunks, kBlock, 0, s>>>(jobs, chunk0s, n_jobs, jobL);
-  return hipGetLastError();
-}
-
-hipError_t launch_full_small_hashed(const FullJobDev* jobs, const uint32_t* wg0s, int n_jobs,
-                                    uint32_t total_wgs, hipStream_t s) {
-  if (total_wgs == 0) return hipSuccess;
-  full_small_hashed_kernel<kSmallBlock><<<total_wgs, kSmallBlock, 0, s>>>(jobs, wg0s, n_jobs);
   return hipGetLastError();
 }
 

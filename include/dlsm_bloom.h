@@ -163,10 +163,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             count then takes a slower per-slice re-hash fallback)
  *   DLSM_OPT_PROBE_ROUND_SERIAL 1: probe rounds run one after another on the context
  *                             stream (one buffer set) instead of pipelined over two
- *                             streams (default 0, or $DLSM_PROBE_SERIAL)
- *   DLSM_OPT_SMALL_BUILD      1: hashed build jobs of at most 4,096 lines (~210 K keys
- *                             at 10 bits/key) build in one launch; 0 (default, or
- *                             $DLSM_SMALL_BUILD): count + partition + slice like large jobs */
+ *                             streams (default 0, or $DLSM_PROBE_SERIAL) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
@@ -174,7 +171,6 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_PROBE_SLICE_LG 4
 #define DLSM_OPT_BUILD_EXACT 5
 #define DLSM_OPT_PROBE_ROUND_SERIAL 6
-#define DLSM_OPT_SMALL_BUILD 7
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 /* The current value of an option (so a caller can restore it). */
 int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);

@@ -307,12 +307,16 @@ int main() {
     dlsm_batcher_destroy(bat);
   }
   // ---- two live builders on ONE context: the second stages into a
-  // private pinned buffer, both filters stay exact ----
-  {
+  // private pinned buffer, both filters stay exact; keys over PCIe, then
+  // hashes (the first streams them to the context's device buffer during
+  // AddKey, the second hands them over in Finish) ----
+  for (int hm = 0; hm < 2; hm++) {
     const int n1 = 40000, n2 = 70000;  // the second grows past the first's size
     std::vector<char> s1(256 * 1024, 0), s2(256 * 1024, 0);
     dlsm_adapter::FilterSlot m1{s1.data(), s1.size()}, m2{s2.data(), s2.size()};
-    dlsm_adapter::FullFilterBlockBuilder b1(&m1, 10, ctx), b2(&m2, 10, ctx);
+    dlsm_adapter::BuilderOptions bo;
+    bo.hash_in_addkey = hm == 1;
+    dlsm_adapter::FullFilterBlockBuilder b1(&m1, 10, ctx, bo), b2(&m2, 10, ctx, bo);
     std::string f1, f2;
     std::vector<uint64_t> o1{0}, o2{0};
     for (int i = 0; i < n2; i++) {  // interleaved, as two tables' iterators would be

@@ -78,34 +78,20 @@ def _runs(orc, seed, n, max_rep):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("small", [True, False])
 @pytest.mark.parametrize("n", [1, 3_000, 153_846, 209_664, 209_665])
-def test_gpu_hashed_small_and_sliced_paths(gpu, orc, small, n):
-    """The one-launch path for small hashed jobs (<= 4,096 lines: n <= 209,664
-    at 10 bits/key) and the count + partition + slice path give the same
-    bytes as the oracle -- at the boundary, with and without repeated keys."""
-    import dlsm_amd
-
-    was = gpu.get_option(dlsm_amd.OPT_SMALL_BUILD)
-    gpu.set_small_build(small)
-    try:
-        keys = orc.dbbench_keys(5, 7, n)
-        assert gpu.full_build_hashed([bloom_hash_k20(keys)])[0] == orc.full_build(keys, n)
-        dup, m = _runs(orc, n, max(1, n // 3), 3)
-        want = orc.full_build(dup, m)
-        assert gpu.full_build_hashed([bloom_hash_k20(dup)])[0] == want
-    finally:
-        gpu.set_option(dlsm_amd.OPT_SMALL_BUILD, was)
+def test_gpu_hashed_runs_of_repeats(gpu, orc, n):
+    """Hash streams with runs of repeated keys (several versions of a user
+    key, one run of 150) give the oracle's bytes from the keys themselves."""
+    keys = orc.dbbench_keys(5, 7, n)
+    assert gpu.full_build_hashed([bloom_hash_k20(keys)])[0] == orc.full_build(keys, n)
+    dup, m = _runs(orc, n, max(1, n // 3), 3)
+    assert gpu.full_build_hashed([bloom_hash_k20(dup)])[0] == orc.full_build(dup, m)
 
 
 @pytest.mark.gpu
 def test_gpu_hashed_small_batch_and_bpk(gpu, orc):
-    """Many small jobs of different sizes in one launch (the batcher's shape),
+    """Many small jobs of different sizes in one call (the batcher's shape),
     including empty and one-hash-repeated jobs, at several bits_per_key."""
-    import dlsm_amd
-
-    was = gpu.get_option(dlsm_amd.OPT_SMALL_BUILD)
-    gpu.set_small_build(True)
     sizes = [0, 1, 2, 63, 64, 65, 1000, 4097, 30_000, 153_846, 200_000]
     for bpk in (1, 6, 10, 16):
         keys = [orc.dbbench_keys(s + 40, 3, n) for s, n in enumerate(sizes)]
@@ -116,57 +102,83 @@ def test_gpu_hashed_small_batch_and_bpk(gpu, orc):
             assert g == orc.full_build(k, n, bpk=bpk), (bpk, n)
         one = np.tile(keys[-2][:20], 5000)
         assert got[-1] == orc.full_build(one, 5000, bpk=bpk)
-    gpu.set_option(dlsm_amd.OPT_SMALL_BUILD, was)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("small", [True, False])
-def test_gpu_hashed_capacity_error(gpu, orc, small):
+def test_gpu_hashed_capacity_error(gpu, orc):
     import dlsm_amd
 
-    was = gpu.get_option(dlsm_amd.OPT_SMALL_BUILD)
-    gpu.set_small_build(small)
-    try:
-        keys = orc.dbbench_keys(0, 1, 5000)
-        need = dlsm_amd.full_size(5000)[0]
-        with pytest.raises(dlsm_amd.DlsmError) as e:
-            gpu.full_build_hashed([bloom_hash_k20(keys)], 10, caps=[need - 1])
-        assert e.value.status == -2
-        assert gpu.full_build_hashed([bloom_hash_k20(keys)], 10, caps=[need])[0] == orc.full_build(keys, 5000)
-    finally:
-        gpu.set_option(dlsm_amd.OPT_SMALL_BUILD, was)
+    keys = orc.dbbench_keys(0, 1, 5000)
+    need = dlsm_amd.full_size(5000)[0]
+    with pytest.raises(dlsm_amd.DlsmError) as e:
+        gpu.full_build_hashed([bloom_hash_k20(keys)], 10, caps=[need - 1])
+    assert e.value.status == -2
+    assert gpu.full_build_hashed([bloom_hash_k20(keys)], 10, caps=[need])[0] == orc.full_build(keys, 5000)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("small", [True, False])
-def test_gpu_hashed_dev_unaligned_hashes(gpu, orc, small):
+def test_gpu_hashed_dev_unaligned_hashes(gpu, orc):
     """Device hashes at every 4-byte offset from a 16-byte boundary, with the
     words just before and after equal to the first / last hash (a sweep that
     read them as neighbours would drop the first hash or add one)."""
     import torch
 
-    import dlsm_amd
-
     n = 20_011
     keys = orc.dbbench_keys(21, 5, n)
     h = bloom_hash_k20(keys).view(np.int32)
     want = orc.full_build(keys, n)
-    was = gpu.get_option(dlsm_amd.OPT_SMALL_BUILD)
-    gpu.set_small_build(small)
+    for off in range(4):
+        host = np.zeros(n + 8, dtype=np.int32)
+        host[off:off + n] = h
+        if off:
+            host[off - 1] = h[0]
+        host[off + n] = h[-1]
+        base = torch.from_numpy(host).cuda()
+        out = torch.zeros(len(want) + 64, dtype=torch.uint8, device="cuda")
+        lens = torch.zeros(1, dtype=torch.uint64, device="cuda")
+        torch.cuda.synchronize()
+        gpu.full_build_hashed_dev([base[off:off + n]], [out], lens)
+        gpu.sync()
+        ln = int(lens.cpu()[0])
+        assert ln == len(want) and bytes(out[:ln].cpu().numpy()) == want, off
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hashed", [False, True])
+def test_gpu_host_build_into_pinned_slots(gpu, orc, hashed):
+    """Host-API builds whose slots are page-locked (the kernels store the
+    filter straight into host memory) or pageable / not 16-byte aligned
+    (page-locked staging, then a copy), side by side in one batch, with the
+    lengths in page-locked memory: one synchronisation per call."""
+    import ctypes as C
+
+    import dlsm_amd
+
+    sizes = [153_846, 0, 77, 40_000]
+    keys = [orc.dbbench_keys(s + 3, 11, n) for s, n in enumerate(sizes)]
+    want = [orc.full_build(k, n) for k, n in zip(keys, sizes)]
+    pins = [dlsm_amd.PinnedArray(dlsm_amd.full_size(n)[0] + 64) for n in sizes]
     try:
-        for off in range(4):
-            host = np.zeros(n + 8, dtype=np.int32)
-            host[off:off + n] = h
-            if off:
-                host[off - 1] = h[0]
-            host[off + n] = h[-1]
-            base = torch.from_numpy(host).cuda()
-            out = torch.zeros(len(want) + 64, dtype=torch.uint8, device="cuda")
-            lens = torch.zeros(1, dtype=torch.uint64, device="cuda")
-            torch.cuda.synchronize()
-            gpu.full_build_hashed_dev([base[off:off + n]], [out], lens)
-            gpu.sync()
-            ln = int(lens.cpu()[0])
-            assert ln == len(want) and bytes(out[:ln].cpu().numpy()) == want, off
+        if hashed:
+            hs = [bloom_hash_k20(k) if n else np.zeros(1, np.uint32) for k, n in zip(keys, sizes)]
+            tabs = [dlsm_amd.Keys(h, n, 4) for h, n in zip(hs, sizes)]
+            fn = dlsm_amd.lib().dlsm_bloom_full_build_hashed
+        else:
+            tabs = [dlsm_amd.Keys(k if n else np.zeros(20, np.uint8), n, 20) for k, n in zip(keys, sizes)]
+            fn = dlsm_amd.lib().dlsm_bloom_full_build
+        for layout in range(2):
+            if layout == 0:  # aligned pinned, pageable, unaligned pinned, aligned pinned
+                outs = [pins[0].array, np.zeros(len(want[1]) + 16, np.uint8), pins[2].array[4:], pins[3].array]
+            else:  # the other way round
+                outs = [pins[0].array[4:], pins[1].array, np.zeros(len(want[2]) + 16, np.uint8), pins[3].array[8:]]
+            for o in outs:
+                o[:] = 0xA5
+            jobs = gpu._jobs(tabs, outs, [len(w) for w in want])
+            lens = (C.c_uint64 * len(sizes))()
+            dlsm_amd.check(fn(gpu.h, jobs, len(sizes), 10, lens), "full_build")
+            for o, w, ln in zip(outs, want, lens):
+                assert ln == len(w) and o[:ln].tobytes() == w, layout
+                assert np.all(o[ln:ln + 4] == 0xA5), layout  # nothing written past the filter
     finally:
-        gpu.set_option(dlsm_amd.OPT_SMALL_BUILD, was)
+        for p in pins:
+            p.close()
