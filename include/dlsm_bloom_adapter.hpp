@@ -195,11 +195,32 @@ inline bool HasAvx512() {
   static const bool has = __builtin_cpu_supports("avx512f");
   return has;
 }
+// AddKey's consecutive-duplicate drop (full_filter_block.cc:45-48) over n
+// hashes, n a multiple of 16: each vector is compared with itself shifted by
+// one hash (the previous hash in front), the kept lanes are compressed
+// together in a register and stored.  Writes up to 64 bytes at out + 4*kept
+// (the caller leaves that much room); returns the number kept.
+__attribute__((target("avx512f"))) inline size_t DedupStore16(const uint32_t* h, size_t n, uint32_t last,
+                                                              bool keep_first, uint8_t* out) {
+  size_t kept = 0;
+  __m512i prev = _mm512_set1_epi32(static_cast<int>(last));
+  for (size_t j = 0; j < n; j += 16) {
+    const __m512i v = _mm512_loadu_si512(h + j);
+    const __m512i pv = _mm512_alignr_epi32(v, prev, 15);  // [prev[15], v[0] .. v[14]]
+    __mmask16 keep = _mm512_cmpneq_epu32_mask(v, pv);
+    if (keep_first && j == 0) keep = static_cast<__mmask16>(keep | 1u);
+    _mm512_storeu_si512(out + 4 * kept, _mm512_maskz_compress_epi32(keep, v));
+    kept += static_cast<size_t>(__builtin_popcount(keep));
+    prev = v;
+  }
+  return kept;
+}
 #else
 inline void BloomHash20x16(const char* p, uint32_t* out) {
   for (int q = 0; q < 4; q++) BloomHash20x4(p + 80 * q, out + 4 * q);
 }
 inline bool HasAvx512() { return false; }
+inline size_t DedupStore16(const uint32_t*, size_t, uint32_t, bool, uint8_t*) { return 0; }
 #endif
 
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
@@ -292,7 +313,9 @@ class FullFilterBlockBuilder {
   FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx, BuilderOptions opt = {})
       : local_mr_(mr), bits_per_key_(bits_per_key),
         num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx), opt_(opt), keys_(ctx),
-        result(static_cast<char*>(mr->addr), 0) {}
+        result(static_cast<char*>(mr->addr), 0) {
+    if (opt_.hash_in_addkey) pend_bytes_.resize(kHashBlock * 32);  // a block of 20-byte keys fits
+  }
   FullFilterBlockBuilder(const FullFilterBlockBuilder&) = delete;
   FullFilterBlockBuilder& operator=(const FullFilterBlockBuilder&) = delete;
 
@@ -310,11 +333,22 @@ class FullFilterBlockBuilder {
       // the block is hashed at once (independent hash chains overlap) and its
       // hashes staged -- the same values, in the same order, as hashing in
       // every AddKey call
+      if (key.size() == 20 && pend_fixed20_) {  // db_bench's shape: two fixed-size copies
+        char* d = pend_bytes_.data() + pend_size_;
+        std::memcpy(d, key.data(), 16);
+        std::memcpy(d + 16, key.data() + 16, 4);
+        pend_size_ += 20;
+        if (++pend_n_ == kHashBlock) hash_pending();
+        return;
+      }
+      if (pend_fixed20_) {  // a key of another length: the pending ones were all 20 bytes
+        for (size_t i = 0; i < pend_n_; i++) pend_len_[i] = 20;
+        pend_fixed20_ = false;
+      }
       if (pend_size_ + key.size() > pend_bytes_.size())
         pend_bytes_.resize(2 * (pend_size_ + key.size()) + kHashBlock * 32);
       std::memcpy(pend_bytes_.data() + pend_size_, key.data(), key.size());
       pend_size_ += key.size();
-      pend_fixed20_ = pend_fixed20_ && key.size() == 20;
       pend_len_[pend_n_++] = static_cast<uint32_t>(key.size());
       if (pend_n_ == kHashBlock) hash_pending();
       return;
@@ -413,7 +447,7 @@ class FullFilterBlockBuilder {
   // equal to its predecessor (full_filter_block.cc:45-48) branch-free: every
   // hash is written, the write position advances only for a kept one.
   void hash_pending() {
-    uint8_t* t = keys_.tail(4 * pend_n_);
+    uint8_t* t = keys_.tail(4 * pend_n_ + 64);  // + a 64-byte vector store's overhang
     if (!t) {
       stage_status_ = DLSM_E_NOMEM;
       pend_size_ = pend_n_ = 0;
@@ -424,24 +458,35 @@ class FullFilterBlockBuilder {
     const char* p = pend_bytes_.data();
     size_t i = 0;
     // 20-byte keys 16 at a time (AVX-512) or four at a time (four
-    // independent multiply chains)
-    if (pend_fixed20_ && HasAvx512())
-      for (; i + 16 <= pend_n_; i += 16, p += 320) BloomHash20x16(p, h + i);
-    for (; i + 4 <= pend_n_ && pend_len_[i] == 20 && pend_len_[i + 1] == 20 && pend_len_[i + 2] == 20 &&
-           pend_len_[i + 3] == 20;
-         i += 4, p += 80)
-      BloomHash20x4(p, h + i);
-    for (; i < pend_n_; i++) {
-      h[i] = BloomHash(p, pend_len_[i]);
-      p += pend_len_[i];
+    // independent multiply chains); pend_len_ is filled only once the block
+    // holds a key of another length
+    if (pend_fixed20_) {
+      if (HasAvx512())
+        for (; i + 16 <= pend_n_; i += 16, p += 320) BloomHash20x16(p, h + i);
+      for (; i + 4 <= pend_n_; i += 4, p += 80) BloomHash20x4(p, h + i);
+      for (; i < pend_n_; i++, p += 20) h[i] = BloomHash(p, 20);
+    } else {
+      for (; i + 4 <= pend_n_ && pend_len_[i] == 20 && pend_len_[i + 1] == 20 && pend_len_[i + 2] == 20 &&
+             pend_len_[i + 3] == 20;
+           i += 4, p += 80)
+        BloomHash20x4(p, h + i);
+      for (; i < pend_n_; i++) {
+        h[i] = BloomHash(p, pend_len_[i]);
+        p += pend_len_[i];
+      }
     }
     size_t kept = 0;
     uint32_t last = last_hash_;
     const bool first = n_ == 0;
-    for (size_t j = 0; j < pend_n_; j++) {
-      std::memcpy(t + 4 * kept, &h[j], 4);
-      kept += static_cast<size_t>((first && j == 0) | (h[j] != last));
-      last = h[j];
+    if (pend_n_ % 16 == 0 && HasAvx512()) {
+      kept = DedupStore16(h, pend_n_, last, first, t);
+      last = h[pend_n_ - 1];
+    } else {
+      for (size_t j = 0; j < pend_n_; j++) {
+        std::memcpy(t + 4 * kept, &h[j], 4);
+        kept += static_cast<size_t>((first && j == 0) | (h[j] != last));
+        last = h[j];
+      }
     }
     keys_.advance(4 * kept);
     n_ += kept;

@@ -73,6 +73,19 @@ def test_adapter_output_capacity_on_cpu(tmp_path):
     assert out.returncode == 0 and "OK adapter host" in out.stdout, out.stdout + out.stderr
 
 
+def test_adapter_addkey_hashing_on_cpu(tmp_path):
+    """hash_in_addkey: the hashes a builder hands to the library are BloomHash
+    of every key minus consecutive repeats (full_filter_block.cc:39-49), over
+    the 20-byte fast path, AVX-512 block hashing + compress-store dedup and the
+    scalar paths, across block boundaries and key-length changes.  The C ABI
+    calls are stubbed in the test (host memory), so it runs without a GPU."""
+    exe = tmp_path / "adapter_addkey_cpu_test"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-fno-rtti", "-fno-exceptions", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "adapter_addkey_cpu_test.cc"), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "OK adapter addkey cpu" in out.stdout, out.stdout + out.stderr
+
+
 @pytest.mark.gpu
 def test_adapter_on_gpu(tmp_path):
     exe = _compile(tmp_path, "adapter_test")
