@@ -128,6 +128,7 @@ def main():
 
     import dlsm_amd
     from dlsm_amd import sharding as SH
+    from dlsm_amd.multigpu import event_stride
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -239,7 +240,13 @@ def main():
     def ev():
         return torch.cuda.Event(enable_timing=True)
 
+    # the passes of every `every`-th timed step are bracketed with events (an
+    # event pair at a call boundary idles the GPU for several microseconds:
+    # timing every step would lengthen the steps being timed,
+    # profiles/r03_o_pass_events_ab.txt)
+    every = event_stride(args.steps)
     evs = [(ev(), ev(), ev(), ev()) for _ in range(0 if use_native else args.steps)]
+    sampled = [i % every == every - 1 for i in range(args.steps)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -249,16 +256,17 @@ def main():
         if graph is not None:
             graph.replay()
             continue
-        if pass_events:
+        tev = pass_events and sampled[i]
+        if tev:
             evs[i][0].record(stream_b)
         if tables:
             ctx_b.full_build_dev(tables, outs, lens, bpk)
-        if pass_events:
+        if tev:
             evs[i][1].record(stream_b)
             evs[i][2].record(stream)
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
-        if pass_events or cosched:
+        if tev or cosched:
             evs[i][3].record(stream)
         if cosched:
             # the next build partition starts behind this probe's slice /
@@ -290,8 +298,10 @@ def main():
             evs[i][3].record(stream)
         stream.synchronize()
     if not use_native:
-        build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
-        probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+        if not pass_events or cosched:
+            sampled = [True] * args.steps  # the instrumented re-run above timed every step
+        build_ms = float(np.mean([e[0].elapsed_time(e[1]) for e, t in zip(evs, sampled) if t]))
+        probe_ms = float(np.mean([e[2].elapsed_time(e[3]) for e, t in zip(evs, sampled) if t]))
 
     # keys of the whole job per step (every rank's share)
     rank_keys = len(tables) * N + qk.n
@@ -338,6 +348,7 @@ def main():
             "overlap": overlap,
             "hip_graph": graph is not None,
             "timed_by": "dlsm_multi_device_run (C++ loop)" if use_native else "Python loop",
+            "pass_events_every": event_stride(args.steps),
             "cosched_build_slice_cus_per_xcd": cosched,
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
@@ -468,6 +479,7 @@ def run_threads(args) -> int:
             "parallelism": (f"strong: {T} SSTables split s mod {N_GPU}, filters replicated, {Q} lookups "
                             f"sharded x{N_GPU}; one process, one host thread + context + stream per GPU"),
             "launch": "threads (dlsm_multi_device_run)",
+            "pass_events_every": MG.event_stride(args.steps),
             "devices": devices,
             "rehearsal": bool(args.rehearse),
             "gpu_tables": [w.work.tables for w in workers],

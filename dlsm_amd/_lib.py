@@ -135,6 +135,8 @@ SIGNATURES = [
     ("dlsm_batcher_stats", C.c_int, [_VP, _U64P, _U64P, _U64P]),
     ("dlsm_multi_device_run", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(C.c_double), C.POINTER(C.c_float)]),
+    ("dlsm_multi_device_run_sampled", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
+                                               C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float)]),
 ]
 
 _LIB = None

@@ -60,9 +60,9 @@ int drain(const dlsm_device_work& w) {
 
 }  // namespace
 
-extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bits_per_key, int steps, int warmup,
-                                     double* wall_seconds, float* pass_ms) {
-  if (!work || n < 1 || steps < 1 || warmup < 0 || !wall_seconds) return DLSM_E_ARG;
+extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n, int bits_per_key, int steps,
+                                             int warmup, int event_every, double* wall_seconds, float* pass_ms) {
+  if (!work || n < 1 || steps < 1 || warmup < 0 || !wall_seconds || event_every < 1) return DLSM_E_ARG;
   for (int d = 0; d < n; d++) {
     const dlsm_device_work& w = work[d];
     if (!w.probe_ctx || !w.build_ctx || (w.n_jobs > 0 && (!w.jobs || !w.out_len_dev))) return DLSM_E_ARG;
@@ -79,7 +79,9 @@ extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bi
       if (hipSetDevice(dlsm_ctx_device(w.probe_ctx)) != hipSuccess) st = DLSM_E_DEVICE;
       for (int i = 0; i < warmup && st == DLSM_OK; i++) st = step(w, bits_per_key);
       if (st == DLSM_OK) st = drain(w);
-      // device 0 brackets each pass with events on the stream it runs on
+      // device 0 brackets each pass of every event_every-th step with events
+      // on the stream it runs on (an event pair at a call boundary leaves the
+      // GPU idle for several microseconds: profiles/r03_o_pass_events_ab.txt)
       const bool events = d == 0 && pass_ms && st == DLSM_OK;
       std::vector<hipEvent_t> ev;
       if (events) {
@@ -87,26 +89,29 @@ extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bi
         for (auto& e : ev)
           if (hipEventCreate(&e) != hipSuccess) st = DLSM_E_DEVICE;
       }
+      auto sampled = [&](int i) { return events && i % event_every == event_every - 1; };
       hipStream_t bs = static_cast<hipStream_t>(dlsm_ctx_stream(w.build_ctx));
       hipStream_t ps = static_cast<hipStream_t>(dlsm_ctx_stream(w.probe_ctx));
       start.wait();  // every device idle; the host clock starts
       for (int i = 0; i < steps && st == DLSM_OK; i++) {
-        if (events) (void)hipEventRecord(ev[4 * i + 0], bs);
+        const bool e = sampled(i);
+        if (e) (void)hipEventRecord(ev[4 * i + 0], bs);
         if (w.n_jobs > 0) st = dlsm_bloom_full_build_dev(w.build_ctx, w.jobs, w.n_jobs, bits_per_key, w.out_len_dev);
-        if (events) {
+        if (e) {
           (void)hipEventRecord(ev[4 * i + 1], bs);
           (void)hipEventRecord(ev[4 * i + 2], ps);
         }
         if (st == DLSM_OK && w.fs && w.keys.n > 0) st = dlsm_bloom_full_probe_dev(w.probe_ctx, w.fs, &w.keys, w.mask_dev);
-        if (events) (void)hipEventRecord(ev[4 * i + 3], ps);
+        if (e) (void)hipEventRecord(ev[4 * i + 3], ps);
       }
       if (st == DLSM_OK) st = drain(w);
       end.wait();  // every device drained; the host clock stops
       if (events) {
         for (int i = 0; i < steps; i++) {
-          float b = 0.f, p = 0.f;
-          if (st == DLSM_OK && (hipEventElapsedTime(&b, ev[4 * i + 0], ev[4 * i + 1]) != hipSuccess ||
-                                hipEventElapsedTime(&p, ev[4 * i + 2], ev[4 * i + 3]) != hipSuccess))
+          float b = -1.f, p = -1.f;  // not sampled
+          if (sampled(i) && st == DLSM_OK &&
+              (hipEventElapsedTime(&b, ev[4 * i + 0], ev[4 * i + 1]) != hipSuccess ||
+               hipEventElapsedTime(&p, ev[4 * i + 2], ev[4 * i + 3]) != hipSuccess))
             st = DLSM_E_DEVICE;
           pass_ms[2 * i] = b;
           pass_ms[2 * i + 1] = p;
@@ -124,4 +129,9 @@ extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bi
   for (int s : status)
     if (s != DLSM_OK) return s;
   return DLSM_OK;
+}
+
+extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bits_per_key, int steps, int warmup,
+                                     double* wall_seconds, float* pass_ms) {
+  return dlsm_multi_device_run_sampled(work, n, bits_per_key, steps, warmup, 1, wall_seconds, pass_ms);
 }

@@ -24,6 +24,9 @@ from dataclasses import dataclass, field
 
 from . import sharding as SH
 
+# timed steps whose passes are bracketed with HIP events (event_stride)
+PASS_EVENT_SAMPLES = 4
+
 
 class DeviceCountError(RuntimeError):
     """More GPUs requested than the node has (and no rehearsal)."""
@@ -115,23 +118,30 @@ class DeviceWorker:
         self.stream_b.synchronize()
 
     def timed_steps(self, k: int):
-        """k steps; with pass_events, HIP events bracket each pass on its stream."""
+        """k steps; with pass_events, HIP events bracket each pass of every
+        event_stride(k)-th step on its stream."""
         import torch
 
         if not self.opts.pass_events:
             for _ in range(k):
                 self.step()
             return
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(k)]
+        every = event_stride(k)
+        evs = []
         for i in range(k):
-            evs[i][0].record(self.stream_b)
+            if i % every != every - 1:
+                self.step()
+                continue
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            e[0].record(self.stream_b)
             if self._build:
                 self._build()
-            evs[i][1].record(self.stream_b)
-            evs[i][2].record(self.stream)
+            e[1].record(self.stream_b)
+            e[2].record(self.stream)
             if self._probe:
                 self._probe()
-            evs[i][3].record(self.stream)
+            e[3].record(self.stream)
+            evs.append(e)
         self._evs = evs
 
     def collect_pass_times(self):
@@ -259,20 +269,29 @@ def device_work(ctx, build_ctx, inp):
     return w, (jobs, w)
 
 
-def native_run(works, steps: int, warmup: int, bits_per_key: int):
-    """dlsm_multi_device_run over dlsm_device_work structs: (seconds,
-    [(build_ms, probe_ms) per step] of the first device)."""
+def event_stride(steps: int, samples: int = PASS_EVENT_SAMPLES) -> int:
+    """Every how many timed steps the passes are bracketed with HIP events:
+    `samples` steps spread over the timed region (each event pair at a call
+    boundary idles the GPU for several microseconds, so timing every step
+    lengthens the very steps being timed: profiles/r03_o_pass_events_ab.txt)."""
+    return max(1, steps // max(1, samples))
+
+
+def native_run(works, steps: int, warmup: int, bits_per_key: int, event_every: int | None = None):
+    """dlsm_multi_device_run_sampled over dlsm_device_work structs: (seconds,
+    [(build_ms, probe_ms) per sampled step] of the first device)."""
     import ctypes as C
 
     from . import _lib as L
     from . import check, lib
 
+    every = event_stride(steps) if event_every is None else event_every
     arr = (L.dlsm_device_work * len(works))(*works)
     wall = C.c_double(0.0)
     pm = (C.c_float * (2 * steps))()
-    check(lib().dlsm_multi_device_run(arr, len(works), bits_per_key, steps, warmup, C.byref(wall), pm),
-          "multi_device_run")
-    return wall.value, [(pm[2 * i], pm[2 * i + 1]) for i in range(steps)]
+    check(lib().dlsm_multi_device_run_sampled(arr, len(works), bits_per_key, steps, warmup, every, C.byref(wall),
+                                              pm), "multi_device_run")
+    return wall.value, [(pm[2 * i], pm[2 * i + 1]) for i in range(steps) if pm[2 * i + 1] >= 0]
 
 
 def native_timed_run(workers, steps: int, warmup: int, bits_per_key: int):

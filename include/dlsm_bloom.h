@@ -449,6 +449,12 @@ typedef struct {
  * step from HIP events on the streams they run on. */
 int dlsm_multi_device_run(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps, int warmup,
                           double* wall_seconds, float* pass_ms);
+/* The same, with entry 0's passes timed on every event_every-th step only
+ * (steps i with i % event_every == event_every - 1); the other steps' pass_ms
+ * entries are -1.  A timed event pair at a call boundary leaves the GPU idle
+ * for several microseconds, so sampling keeps the timed steps' shape. */
+int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps,
+                                  int warmup, int event_every, double* wall_seconds, float* pass_ms);
 
 /* ---- measurement helper (not on the filter path) ------------------------ */
 

@@ -43,6 +43,21 @@ def test_device_map_rules():
         MG.device_map(2, True, 0)
 
 
+def test_pass_events_are_sampled():
+    """The timed steps carry per-pass HIP events on only PASS_EVENT_SAMPLES of
+    them (an event pair at a call boundary idles the GPU for microseconds:
+    profiles/r03_o_pass_events_ab.txt), spread over the timed region."""
+    from dlsm_amd import multigpu as MG
+
+    assert MG.PASS_EVENT_SAMPLES == 4
+    for steps in (1, 3, 4, 20, 100, 101):
+        every = MG.event_stride(steps)
+        sampled = [i for i in range(steps) if i % every == every - 1]
+        assert 1 <= len(sampled) <= max(4, steps // every)
+        assert sampled[-1] >= steps - every  # the region's end is sampled too
+    assert MG.event_stride(20) == 5 and MG.event_stride(3) == 1
+
+
 def test_too_many_gpus_exits_nonzero():
     """No silent one-GPU run: --gpus 8 where fewer GPUs are visible fails."""
     import torch
