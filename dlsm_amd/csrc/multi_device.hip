@@ -11,7 +11,6 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
-#include <cstdlib>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -69,11 +68,6 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
     if (!w.probe_ctx || !w.build_ctx || (w.n_jobs > 0 && (!w.jobs || !w.out_len_dev))) return DLSM_E_ARG;
     if (dlsm_ctx_device(w.probe_ctx) != dlsm_ctx_device(w.build_ctx)) return DLSM_E_ARG;
   }
-  // A/B: issue each step's probe before its build ($DLSM_STEP_PROBE_FIRST=1)
-  static const bool probe_first = [] {
-    const char* v = getenv("DLSM_STEP_PROBE_FIRST");
-    return v && atoi(v) != 0;
-  }();
   Barrier start(n + 1), end(n + 1);
   std::vector<int> status(n, DLSM_OK);
   std::vector<std::thread> threads;
@@ -101,23 +95,14 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
       start.wait();  // every device idle; the host clock starts
       for (int i = 0; i < steps && st == DLSM_OK; i++) {
         const bool e = sampled(i);
-        auto build = [&] {
-          if (e) (void)hipEventRecord(ev[4 * i + 0], bs);
-          if (w.n_jobs > 0) st = dlsm_bloom_full_build_dev(w.build_ctx, w.jobs, w.n_jobs, bits_per_key, w.out_len_dev);
-          if (e) (void)hipEventRecord(ev[4 * i + 1], bs);
-        };
-        auto probe = [&] {
-          if (e) (void)hipEventRecord(ev[4 * i + 2], ps);
-          if (st == DLSM_OK && w.fs && w.keys.n > 0) st = dlsm_bloom_full_probe_dev(w.probe_ctx, w.fs, &w.keys, w.mask_dev);
-          if (e) (void)hipEventRecord(ev[4 * i + 3], ps);
-        };
-        if (probe_first) {
-          probe();
-          if (st == DLSM_OK) build();
-        } else {
-          build();
-          if (st == DLSM_OK) probe();
+        if (e) (void)hipEventRecord(ev[4 * i + 0], bs);
+        if (w.n_jobs > 0) st = dlsm_bloom_full_build_dev(w.build_ctx, w.jobs, w.n_jobs, bits_per_key, w.out_len_dev);
+        if (e) {
+          (void)hipEventRecord(ev[4 * i + 1], bs);
+          (void)hipEventRecord(ev[4 * i + 2], ps);
         }
+        if (st == DLSM_OK && w.fs && w.keys.n > 0) st = dlsm_bloom_full_probe_dev(w.probe_ctx, w.fs, &w.keys, w.mask_dev);
+        if (e) (void)hipEventRecord(ev[4 * i + 3], ps);
       }
       if (st == DLSM_OK) st = drain(w);
       end.wait();  // every device drained; the host clock stops
