@@ -600,7 +600,11 @@ struct SegWalk {
   // past-the-end groups to the last chunk): a prefetch under a branch makes
   // the compiler merge the two values of nrow with a copy that waits
   // (s_waitcnt vmcnt(0)) right after the load is issued.
-  __device__ __forceinline__ bool start(uint32_t g_first) {
+  // begin() issues the first group's row loads (and the next group's) and
+  // returns the first row pair without waiting for it; start() hands it to
+  // setup().  A caller with a prologue of its own runs it in between, so the
+  // row loads' round trip overlaps it.
+  __device__ __forceinline__ bool begin(uint32_t g_first, uint32_t& row) {
     g = g_first;
     if (g >= g_end) return false;
     if constexpr (U <= 2) {
@@ -608,8 +612,13 @@ struct SegWalk {
       for (int u = 0; u < kFlags / 64; u++) scr[u * 64 + (threadIdx.x & 63)] = ~0u;
       tag = 0;
     }
-    const uint32_t row = load_rows(g);
+    row = load_rows(g);
     nrow = load_rows(g + g_step);
+    return true;
+  }
+  __device__ __forceinline__ bool start(uint32_t g_first) {
+    uint32_t row;
+    if (!begin(g_first, row)) return false;
     setup(row);
     return true;
   }
@@ -665,14 +674,27 @@ struct WinSet {
   bool ok[U];
 };
 
-template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL = false, typename Act>
+struct NoPrologue {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// pro(): the caller's prologue (e.g. its slice image into LDS + a barrier),
+// run by every wave after the first row loads are issued and before they are
+// used -- their round trip overlaps it.  Every wave runs it, walk or not, so
+// it may hold workgroup barriers.
+template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL = false, typename Act,
+          typename Pro = NoPrologue>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
-                                              uint32_t* scratch, Act act) {
+                                              uint32_t* scratch, Act act, Pro pro = Pro{}) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
   SegWalk<U, CHUNK, E, NTL> w{tb, entries, rowlen, g_step, g_end, gs};
   w.scr = (lds_u32*)scratch;  // generic -> LDS address space (addrspacecast)
-  if (!w.start(g_first)) return;
+  uint32_t row0 = 0;
+  const bool any = w.begin(g_first, row0);
+  pro();
+  if (!any) return;
+  w.setup(row0);
   WinSet<U, CHUNK, E> A, B;
   if (!w.next(A.idx, A.ok, A.g)) return;
   w.fetch(A.idx, A.g, A.hv);
@@ -1358,33 +1380,23 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t p = wi / S;
   const uint32_t lo_line = s * Rs;
   const uint32_t nl = min(Rs, L - lo_line);
-  {
-    // all of the slice's 16-byte loads in flight before the first LDS store.
-    // Loads AND stores are clamped (lanes past the slice rewrite its last
-    // unit with the same bytes): a store under a branch let the compiler sink
-    // each load into its branch, one HBM round trip per load.
-    constexpr int V = R * (LB / 16) / NT;
-    const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * LB);
-    uint4* dst = reinterpret_cast<uint4*>(sl);
-    const uint32_t nw = nl * (LB / 16);
-    uint4 t[V];
-#pragma unroll
-    for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
-#pragma unroll
-    for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
-  }
+  // The slice into LDS: every 16-byte load in flight before the first LDS
+  // store.  Loads AND stores are clamped (lanes past the slice rewrite its
+  // last unit with the same bytes): a store under a branch let the compiler
+  // sink each load into its branch, one HBM round trip per load.
+  constexpr int V = R * (LB / 16) / NT;
+  const uint4* src = reinterpret_cast<const uint4*>(stacked + static_cast<uint64_t>(lo_line) * LB);
+  uint4* dst = reinterpret_cast<uint4*>(sl);
+  const uint32_t nw = nl * (LB / 16);
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
-  __syncthreads();
   constexpr uint32_t CRU = probe_region(C) / 4;  // chunk region stride in 16-byte units
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
   const uint32_t gs = min(64u, max(1u, (c_hi - c_lo + NW - 1) / NW));  // chunks per wave group
-  walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
-      tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch,
-      [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
+  auto probe_set = [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
         uint32_t ans[U];
 #pragma unroll
@@ -1439,7 +1451,36 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
         // agree on the count).
 #pragma unroll
         for (int u = 0; u < U; u++) gmask[idx[u]] = ans[u];
-      });
+  };
+  if constexpr (LGW == 3) {
+    // byte-wide images: the slice load runs as the walk's prologue, after the
+    // walk's first table-row loads are issued (one round trip fewer before
+    // the first entries load: small batches)
+    auto slice_to_lds = [&] {
+      uint4 t[V];
+#pragma unroll
+      for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
+#pragma unroll
+      for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
+      __syncthreads();
+    };
+    walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
+        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
+        slice_to_lds);
+  } else {
+    // packed images: the same load in front of the walk (as the walk's
+    // prologue the compiler kept t[] in scratch for these shapes)
+    {
+      uint4 t[V];
+#pragma unroll
+      for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
+#pragma unroll
+      for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
+    }
+    __syncthreads();
+    walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
+        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set);
+  }
 }
 
 // Eight positions (16 bytes) of the unpermute: read once, non-temporal with
@@ -1472,19 +1513,32 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
   // the chunk's answer region (bucket padding included; positions point into it)
   const uint32_t nvec = (min(CR, nk + 4u * kMaxSlices) + 15u) / 16u;
   const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(blockIdx.x) * CR);
+  // the chunk's positions are loaded first (they do not depend on the staged
+  // answers): their round trip overlaps the answers' instead of following it
+  constexpr int PI = C / (8 * kBlock);
+  static_assert(C % (8 * kBlock) == 0, "whole position vectors per thread");
+  uint4 pre[PI];
+#pragma unroll
+  for (int q = 0; q < PI; q++) {
+    const uint32_t i0 = 8u * (static_cast<uint32_t>(q) * kBlock + tid);
+    if (i0 + 8u <= nk) pre[q] = load_pos8(pos + first + i0);
+  }
   for (uint32_t v = tid; v < nvec; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
   __syncthreads();
-  for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
+#pragma unroll
+  for (int q = 0; q < PI; q++) {
+    const uint32_t i0 = 8u * (static_cast<uint32_t>(q) * kBlock + tid);
+    if (i0 >= nk) break;
     if (i0 + 8u <= nk) {
-      const uint4 pv = load_pos8(pos + first + i0);
+      const uint4 pv = pre[q];
       const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
       uint32_t lo = 0, hi = 0;
 #pragma unroll
-      for (int q = 0; q < 2; q++) {
-        lo |= uint32_t(sm[pw[q] & 0xffffu]) << (16 * q);
-        lo |= uint32_t(sm[pw[q] >> 16]) << (16 * q + 8);
-        hi |= uint32_t(sm[pw[q + 2] & 0xffffu]) << (16 * q);
-        hi |= uint32_t(sm[pw[q + 2] >> 16]) << (16 * q + 8);
+      for (int j = 0; j < 2; j++) {
+        lo |= uint32_t(sm[pw[j] & 0xffffu]) << (16 * j);
+        lo |= uint32_t(sm[pw[j] >> 16]) << (16 * j + 8);
+        hi |= uint32_t(sm[pw[j + 2] & 0xffffu]) << (16 * j);
+        hi |= uint32_t(sm[pw[j + 2] >> 16]) << (16 * j + 8);
       }
       if constexpr (VEC) {
         *reinterpret_cast<uint2*>(mask + first + i0) = make_uint2(lo, hi);
