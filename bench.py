@@ -45,7 +45,6 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 # kernels are latency-bound), so the step runs build and probe on two streams:
 # +4 / +9 / +18 % per step at 12.8 / 6.4 / 3.2 M build keys, within +-1 % at
 # the full 25.6 M (profiles/r02_overlap_shares.txt).
-OVERLAP_BELOW = 16_000_000
 
 
 def log(*a):
@@ -92,8 +91,8 @@ def main():
                     help="threads of the all-cores CPU baseline (0 = every host core)")
     ap.add_argument("--cpu-probe-sample", type=int, default=10_000_000)
     ap.add_argument("--overlap", choices=["auto", "on", "off"], default="auto",
-                    help="run the step's build and probe on two streams (auto: when this rank's build batch "
-                         f"is under {OVERLAP_BELOW // 1_000_000} M keys)")
+                    help="run the step's build and probe on two streams (auto = on whenever the rank has "
+                         "both; off = one stream, one pass after the other)")
     ap.add_argument("--cosched", type=int, default=0,
                     help="co-schedule build and probe on CU-masked streams: the build's slice pass on this "
                          "many CUs per XCD (1..4), every partition pass on the other CUs (0 = off)")
@@ -179,8 +178,7 @@ def main():
     # the build's context and stream: a second pair when the step overlaps
     # the build with the probe (their buffers are disjoint: the probe reads
     # the stacked filter set, the build writes the SSTable slots)
-    overlap = bool(tables) and qk.n > 0 and (
-        args.overlap == "on" or (args.overlap == "auto" and len(tables) * N < OVERLAP_BELOW))
+    overlap = bool(tables) and qk.n > 0 and args.overlap != "off"
     cosched = args.cosched if (tables and qk.n > 0) else 0
     part_stream = None
     if cosched:
@@ -247,6 +245,7 @@ def main():
     every = event_stride(args.steps)
     evs = [(ev(), ev(), ev(), ev()) for _ in range(0 if use_native else args.steps)]
     sampled = [i % every == every - 1 for i in range(args.steps)]
+    gate = torch.cuda.Event()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -258,16 +257,23 @@ def main():
             continue
         tev = pass_events and sampled[i]
         if tev:
+            if overlap:  # a sampled step runs its passes alone (as dlsm_multi_device_run_sampled)
+                gate.record(stream)
+                stream_b.wait_event(gate)
             evs[i][0].record(stream_b)
         if tables:
             ctx_b.full_build_dev(tables, outs, lens, bpk)
         if tev:
             evs[i][1].record(stream_b)
+            if overlap:
+                stream.wait_event(evs[i][1])
             evs[i][2].record(stream)
         if qk.n:
             ctx.full_probe_dev(fs, qk, mask)
         if tev or cosched:
             evs[i][3].record(stream)
+        if tev and overlap:
+            stream_b.wait_event(evs[i][3])
         if cosched:
             # the next build partition starts behind this probe's slice /
             # unpermute passes (co-running with them slows both)
@@ -356,6 +362,8 @@ def main():
             "bound": "hbm", "kernel": f"{dominant} pass (rank 0's share)", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
+            **pass_timing_note(overlap, every),
+            **step_roofline(probe_bytes + build_bytes, elapsed / args.steps),
         },
         "host_enqueue_ms_per_step": None if use_native else round(enqueue_s / args.steps * 1e3, 4),
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
@@ -389,8 +397,8 @@ def main():
         result["build"]["rotating_batches_ms"] = round(rotating_build_ms(ctx, stream, tables, outs, lens, bpk), 4)
         # the other step shape (two streams if the timed step was sequential):
         # recorded beside `value`
-        result["overlap_step"] = overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, local,
-                                         elapsed / args.steps)
+        result["other_step_shape"] = other_shape_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk,
+                                                      local, elapsed / args.steps, overlap)
 
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if world == 1 and rank == 0 and not args.no_cpu:
@@ -432,7 +440,7 @@ def run_threads(args) -> int:
     t_in = time.time()
     stream_vals = W.mt19937_64(1000, Q) % np.uint64(2 * F * N)  # the ONE lookup stream, generated once
     opts = MG.WorkerOptions(path=args.path, probe_chunk_lg=args.probe_chunk_lg, probe_slice_lg=args.probe_slice_lg,
-                            overlap=args.overlap, overlap_below=OVERLAP_BELOW, pass_events=True)
+                            overlap=args.overlap, pass_events=True)
     workers = MG.build_workers(N_GPU, devices, T, N, Q, F, bpk, opts, lookup_stream=stream_vals)
     digests = {w.filter_digest() for w in workers}
     if len(digests) != 1:
@@ -492,6 +500,8 @@ def run_threads(args) -> int:
             "bound": "hbm", "kernel": f"{dominant} pass (GPU 0's share)", "achieved": round(ach, 1),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
+            **pass_timing_note(w0.overlap, MG.event_stride(args.steps)),
+            **step_roofline(probe_bytes + build_bytes, elapsed / args.steps),
         },
         "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
                   "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
@@ -656,22 +666,43 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
     return out
 
 
-def overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, device, seq_step_s, reps=10):
-    """Steps whose build runs on a second context/stream while the probe runs
-    on the first (their buffers are disjoint: the probe reads the stacked
-    filter set, the build writes the SSTable slots)."""
+def pass_timing_note(overlapped: bool, every: int) -> dict:
+    """How the pass times behind `achieved` were taken."""
+    how = (f"HIP events around each pass of every {every}-th timed step; those steps run their two passes "
+           "one after the other, alone on the GPU (the other steps overlap the build with the probe on two "
+           "streams), so `achieved` is the pass's own rate" if overlapped else
+           f"HIP events around each pass of every {every}-th timed step (one stream)")
+    return {"pass_timing": how}
+
+
+def step_roofline(step_alg_bytes: float, step_s: float) -> dict:
+    """The whole step's algorithmic bytes (build 21.25 + probe 21.16 B/key,
+    SURVEY.md §8d) over the step time: with the two passes co-running this is
+    the rate the GPU sustains on the job, beside the dominant pass's own."""
+    gbs = step_alg_bytes / step_s / 1e9
+    return {"step_alg_GBs": round(gbs, 1), "step_frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+
+def other_shape_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, device, timed_step_s, overlapped,
+                     reps=10):
+    """The step in the shape the timed region did not use -- one pass after
+    the other on one stream when the timed steps overlapped the build (second
+    context and stream) with the probe, and the overlapped shape otherwise;
+    recorded beside `value`, never `value`."""
     import torch
 
     import dlsm_amd
 
     if not tables or not qk.n:
         return None
-    ctx2 = dlsm_amd.Context(device)
-    ctx2.set_path(args.path)
-    ctx2.set_build_groups(args.build_groups)
-    ctx2.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
-    s2 = torch.cuda.Stream(device=torch.device("cuda", device))
-    ctx2.set_stream(s2)
+    ctx2, s2 = ctx, stream
+    if not overlapped:
+        ctx2 = dlsm_amd.Context(device)
+        ctx2.set_path(args.path)
+        ctx2.set_build_groups(args.build_groups)
+        ctx2.set_probe_shape(args.probe_chunk_lg, args.probe_slice_lg)
+        s2 = torch.cuda.Stream(device=torch.device("cuda", device))
+        ctx2.set_stream(s2)
 
     def one():
         ctx2.full_build_dev(tables, outs, lens, bpk)
@@ -687,12 +718,14 @@ def overlap_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk, devic
     stream.synchronize()
     s2.synchronize()
     dt = (time.perf_counter() - t0) / reps
-    ctx2.sync()
-    del ctx2
+    if not overlapped:
+        ctx2.sync()
+        del ctx2
     nk = len(tables) * tables[0].n + qk.n
-    return {"mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 4),
-            "vs_timed_step": round(seq_step_s / dt, 3),
-            "note": "build on a second stream concurrent with the probe; not `value`"}
+    shape = "build and probe one after the other on one stream" if overlapped else \
+        "build on a second stream concurrent with the probe"
+    return {"shape": shape, "mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 4),
+            "this_vs_timed_step": round(dt / timed_step_s, 3), "note": "not `value`"}
 
 
 def rotating_build_ms(ctx, stream, tables, outs, lens, bpk, reps=10):

@@ -79,30 +79,47 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
       if (hipSetDevice(dlsm_ctx_device(w.probe_ctx)) != hipSuccess) st = DLSM_E_DEVICE;
       for (int i = 0; i < warmup && st == DLSM_OK; i++) st = step(w, bits_per_key);
       if (st == DLSM_OK) st = drain(w);
-      // device 0 brackets each pass of every event_every-th step with events
+      // Device 0 brackets each pass of every event_every-th step with events
       // on the stream it runs on (an event pair at a call boundary leaves the
-      // GPU idle for several microseconds: profiles/r03_o_pass_events_ab.txt)
+      // GPU idle for several microseconds: profiles/r03_o_pass_events_ab.txt).
+      // With the build on a stream of its own, a sampled step runs its passes
+      // alone -- its build after the probes before it, its probe after its
+      // build, the next build after its probe -- so the events time each pass
+      // by itself (the roofline's kernel time), not beside the other.
       const bool events = d == 0 && pass_ms && st == DLSM_OK;
       std::vector<hipEvent_t> ev;
+      hipEvent_t gate = nullptr;
       if (events) {
         ev.resize(4 * static_cast<size_t>(steps));
         for (auto& e : ev)
           if (hipEventCreate(&e) != hipSuccess) st = DLSM_E_DEVICE;
+        if (hipEventCreateWithFlags(&gate, hipEventDisableTiming) != hipSuccess) st = DLSM_E_DEVICE;
       }
       auto sampled = [&](int i) { return events && i % event_every == event_every - 1; };
       hipStream_t bs = static_cast<hipStream_t>(dlsm_ctx_stream(w.build_ctx));
       hipStream_t ps = static_cast<hipStream_t>(dlsm_ctx_stream(w.probe_ctx));
+      const bool two = bs != ps;
       start.wait();  // every device idle; the host clock starts
       for (int i = 0; i < steps && st == DLSM_OK; i++) {
         const bool e = sampled(i);
-        if (e) (void)hipEventRecord(ev[4 * i + 0], bs);
+        if (e) {
+          if (two) {
+            (void)hipEventRecord(gate, ps);
+            (void)hipStreamWaitEvent(bs, gate, 0);
+          }
+          (void)hipEventRecord(ev[4 * i + 0], bs);
+        }
         if (w.n_jobs > 0) st = dlsm_bloom_full_build_dev(w.build_ctx, w.jobs, w.n_jobs, bits_per_key, w.out_len_dev);
         if (e) {
           (void)hipEventRecord(ev[4 * i + 1], bs);
+          if (two) (void)hipStreamWaitEvent(ps, ev[4 * i + 1], 0);
           (void)hipEventRecord(ev[4 * i + 2], ps);
         }
         if (st == DLSM_OK && w.fs && w.keys.n > 0) st = dlsm_bloom_full_probe_dev(w.probe_ctx, w.fs, &w.keys, w.mask_dev);
-        if (e) (void)hipEventRecord(ev[4 * i + 3], ps);
+        if (e) {
+          (void)hipEventRecord(ev[4 * i + 3], ps);
+          if (two) (void)hipStreamWaitEvent(bs, ev[4 * i + 3], 0);
+        }
       }
       if (st == DLSM_OK) st = drain(w);
       end.wait();  // every device drained; the host clock stops
@@ -117,6 +134,7 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
           pass_ms[2 * i + 1] = p;
         }
         for (auto& e : ev) (void)hipEventDestroy(e);
+        if (gate) (void)hipEventDestroy(gate);
       }
     });
   }

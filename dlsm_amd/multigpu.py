@@ -53,8 +53,7 @@ class WorkerOptions:
     path: int = 0
     probe_chunk_lg: int = 13
     probe_slice_lg: int = 8
-    overlap: str = "auto"        # build on a second stream: auto (small shares) | on | off
-    overlap_below: int = 16_000_000
+    overlap: str = "auto"        # build on a second stream: auto (= on when both passes run) | on | off
     pass_events: bool = False    # record per-pass HIP events (device 0's worker)
 
 
@@ -99,9 +98,7 @@ class DeviceWorker:
         self.inp = SH.make_inputs(self.ctx, self.work, self.N, self.F, self.bpk, dev, stream=self.stream,
                                   dist=None, lookup_shard=self.lookup_values)
         inp = self.inp
-        self.overlap = bool(inp.tables) and inp.lookups.n > 0 and (
-            self.opts.overlap == "on" or (self.opts.overlap == "auto"
-                                          and len(inp.tables) * self.N < self.opts.overlap_below))
+        self.overlap = bool(inp.tables) and inp.lookups.n > 0 and self.opts.overlap != "off"
         self.ctx_b, self.stream_b = make_ctx() if self.overlap else (self.ctx, self.stream)
         self._build = (self.ctx_b.bind_full_build_dev(inp.tables, inp.outs, inp.lens, self.bpk)
                        if inp.tables else None)
@@ -132,15 +129,27 @@ class DeviceWorker:
             if i % every != every - 1:
                 self.step()
                 continue
+            # a sampled step runs its passes alone: its build after the probes
+            # before it, its probe after its build, the next build after its
+            # probe (dlsm_multi_device_run_sampled does the same)
             e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            two = self.stream_b is not self.stream
+            if two:
+                gate = torch.cuda.Event()
+                gate.record(self.stream)
+                self.stream_b.wait_event(gate)
             e[0].record(self.stream_b)
             if self._build:
                 self._build()
             e[1].record(self.stream_b)
+            if two:
+                self.stream.wait_event(e[1])
             e[2].record(self.stream)
             if self._probe:
                 self._probe()
             e[3].record(self.stream)
+            if two:
+                self.stream_b.wait_event(e[3])
             evs.append(e)
         self._evs = evs
 

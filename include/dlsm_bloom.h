@@ -452,7 +452,10 @@ int dlsm_multi_device_run(const dlsm_device_work* work, int n_devices, int bits_
 /* The same, with entry 0's passes timed on every event_every-th step only
  * (steps i with i % event_every == event_every - 1); the other steps' pass_ms
  * entries are -1.  A timed event pair at a call boundary leaves the GPU idle
- * for several microseconds, so sampling keeps the timed steps' shape. */
+ * for several microseconds, so sampling keeps the timed steps' shape.  When
+ * entry 0's build runs on its own stream (build_ctx != probe_ctx), a sampled
+ * step runs its two passes one after the other, alone on the device, so
+ * pass_ms holds each pass's own time rather than its time beside the other. */
 int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps,
                                   int warmup, int event_every, double* wall_seconds, float* pass_ms);
 

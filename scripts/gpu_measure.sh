@@ -2,7 +2,8 @@
 # One measuring GPU session: parity tests, rocprofv3 PMC passes (one counter
 # group per run, --kernel-trace only) -> per-launch traffic summary, the full
 # bench line (cpu_baseline + e2e + traffic), and a rocprofv3 kernel-trace
-# --stats summary of the same bench command.  Each GPU step has its own time
+# --stats summary of the same bench command, with the kernels of the steps
+# whose passes the bench times (scripts/sampled_kernel_stats.py).  Each GPU step has its own time
 # limit; the steps are chained with && so the first failure ends the session.
 #   scripts/gpu_measure.sh OUTDIR [extra bench args...]
 set -o pipefail
@@ -27,4 +28,5 @@ python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json"
 timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
   python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --traffic "$OUT/traffic.json" $BARGS \
-  > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err"
+  > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
+python3 scripts/sampled_kernel_stats.py "$OUT/prof" 10 > "$OUT/sampled_kernel_stats.txt"

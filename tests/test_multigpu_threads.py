@@ -86,7 +86,7 @@ _T, _N, _Q, _F = 16, 20_000, 1_000_003, 8
 def test_two_logical_devices_strong_scaling_parity(orc):
     from dlsm_amd import multigpu as MG
 
-    opts = MG.WorkerOptions(overlap="auto", overlap_below=16_000_000, pass_events=True)
+    opts = MG.WorkerOptions(overlap="auto", pass_events=True)
     workers = MG.build_workers(2, [0, 0], _T, _N, _Q, _F, 10, opts,
                                lookup_stream=orc.mt_values(1000, 2 * _F * _N, _Q))
     try:
