@@ -101,7 +101,7 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="--gpus N in one process on a box with fewer GPUs: N logical devices on GPU 0")
     ap.add_argument("--python-loop", action="store_true",
-                    help="N = 1: issue the timed steps from a Python loop instead of the native runner")
+                    help="issue the timed steps from a Python loop instead of the native runner")
     ap.add_argument("--native", action="store_true",
                     help="time the steps with the library's native runner (dlsm_multi_device_run) at any N "
                          "(the default for --gpus N > 1; at N = 1 the Python loop is the default)")
@@ -210,13 +210,18 @@ def main():
     # Python loop (HIP graph, co-scheduling, probe rounds, build groups) or
     # --python-loop asks for it; the Python loop costs 3 % of the step on
     # these boxes (profiles/r03_d_native_shares.txt vs r03_a_bench.json).
-    use_native = (world == 1 and not args.python_loop and not args.graph and not cosched
+    # Under a launcher (one process per GPU) each rank times its own GPU's
+    # steps with the same runner, between a barrier and the max over ranks.
+    use_native = (not args.python_loop and not args.graph and not cosched
                   and args.probe_round is None and not args.probe_serial and not args.build_groups)
     if use_native:
         from dlsm_amd import multigpu as MG
 
         dwork, _keep = MG.device_work(ctx, ctx_b, inp)
+        if dist:
+            dist.barrier()
         elapsed, passes = MG.native_run([dwork], args.steps, args.warmup, bpk)
+        elapsed = SH.max_over_ranks(elapsed, dist, dev)
         build_ms = float(np.mean([b for b, _ in passes]))
         probe_ms = float(np.mean([p for _, p in passes]))
         enqueue_s = float("nan")

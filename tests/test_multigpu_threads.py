@@ -147,3 +147,34 @@ def test_bench_one_gpu_native_and_python_loop():
         assert line["n_gpus"] == 1 and line["config"]["timed_by"].startswith(timed_by)
         assert line["value"] > 0 and line["probe"]["ms"] > 0 and line["build"]["ms"] > 0
         assert line["roofline"]["hbm_read_GBs_measured"] > 1000
+
+
+@pytest.mark.gpu
+def test_bench_under_launcher_two_ranks_rehearsed():
+    """The driver's N > 1 launch: torch.distributed.run, one process per GPU.
+    Rehearsed as two gloo ranks sharing GPU 0 (LOCAL_RANK mod device count):
+    each rank times its share with the native runner between a barrier and
+    the max over ranks; rank 0 prints one line for both."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        e.pop(k, None)
+    e["DLSM_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--keys-per-table", "200000",
+                        "--lookups", "4000000", "--no-cpu", "--no-e2e"],
+                       capture_output=True, text=True, timeout=600, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["timed_by"].startswith("dlsm_multi_device_run")
+    assert line["config"]["rank0_tables"] == list(range(0, 16, 2))
+    assert line["config"]["rank0_lookups"] == 2_000_000
+    assert line["value"] > 0 and line["probe"]["ms"] > 0 and line["build"]["ms"] > 0
