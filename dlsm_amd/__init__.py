@@ -35,7 +35,6 @@ INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbforma
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
-OPT_PROBE_ENTRY_BYTES = 7
 
 
 def lib():
@@ -296,12 +295,6 @@ class Context:
     def set_build_groups(self, groups: int):
         """Job groups of a pipelined build (0 = auto, 1..4)."""
         self.set_option(OPT_BUILD_GROUPS, groups)
-
-    def set_probe_entry_bytes(self, n: int):
-        """3 (default: 3-byte bucketed entries where the shape allows) or 4
-        (DLSM_OPT_PROBE_ENTRY_BYTES).  Scheduling of bytes only: answers never
-        depend on it."""
-        self.set_option(OPT_PROBE_ENTRY_BYTES, n)
 
     def set_build_exact(self, mode: int):
         """0 auto, 1 count distinct hashes before bucketing, 2 never (DLSM_OPT_BUILD_EXACT)."""

@@ -105,7 +105,6 @@ struct dlsm_ctx {
   uint64_t probe_round = 0;  // keys per probe round (0 = whole batch)
   int probe_lgc = 13;        // log2 keys per probe partition chunk (12..14; 13 = two 4,096-key units, 512 threads)
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
-  int probe_eb = 3;          // DLSM_OPT_PROBE_ENTRY_BYTES (3 where the shape allows it)
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
   // build workspace
@@ -403,7 +402,6 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (const char* v = getenv("DLSM_PROBE_ROUND_KEYS")) ctx->probe_round = strtoull(v, nullptr, 10);
   if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
-  if (const char* v = getenv("DLSM_PROBE_ENTRY_BYTES")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_ENTRY_BYTES, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SERIAL")) ctx->probe_serial = atoi(v) != 0;
   *out = ctx;
   return DLSM_OK;
@@ -521,10 +519,6 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value < 7 || value > 8) return DLSM_E_ARG;
       ctx->probe_lgr = static_cast<int>(value);
       return DLSM_OK;
-    case DLSM_OPT_PROBE_ENTRY_BYTES:
-      if (value != 3 && value != 4) return DLSM_E_ARG;
-      ctx->probe_eb = static_cast<int>(value);
-      return DLSM_OK;
     case DLSM_OPT_BUILD_EXACT:
       if (value > 2) return DLSM_E_ARG;
       ctx->build_exact = static_cast<int>(value);
@@ -548,7 +542,6 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_PROBE_SLICE_LG: *value = static_cast<uint64_t>(ctx->probe_lgr); return DLSM_OK;
     case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
     case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
-    case DLSM_OPT_PROBE_ENTRY_BYTES: *value = static_cast<uint64_t>(ctx->probe_eb); return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -1490,10 +1483,7 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
   const uint32_t nCmax = ceil_div_u32(std::min(round, n), C);
   const uint64_t kstride = static_cast<uint64_t>(nCmax) * C;  // keys per buffer (16-B aligned)
   const uint64_t rstride = static_cast<uint64_t>(nCmax) * probe_region(static_cast<uint32_t>(C));  // entries / answers
-  // 3-byte entries where the shape allows (DLSM_OPT_PROBE_ENTRY_BYTES): 4 S + 4
-  // u16 table rows (sub-bucket starts), 3 of the region's 4 bytes per slot
-  const bool e3 = ctx->probe_eb == 3 && probe_e3_supported(S, lgC, mode, grp.lgw, lgR);
-  const uint64_t tstride = static_cast<uint64_t>(e3 ? 4 * S + 4 : S + 1) * nCmax;  // table u16 per buffer
+  const uint64_t tstride = static_cast<uint64_t>(S + 1) * nCmax;        // table u16 per buffer
   DLSM_CHECK(ctx->entries.ensure(rstride * nbuf));
   DLSM_CHECK(ctx->pos.ensure(kstride * nbuf));
   DLSM_CHECK(ctx->smask.ensure(rstride * nbuf));
@@ -1519,11 +1509,11 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     else kr.bytes = kd.bytes + r0 * kd.key_len;
     if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
     DLSM_TRY(launch_probe_partition(kr, grp.L, grp.magic, R, S, ent, pos, tab, mode, lgC, ps,
-                                    split ? ctx->pcus : 0u, e3));
+                                    split ? ctx->pcus : 0u));
     if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
     if (split) DLSM_CHECK(join_part(ctx));
     DLSM_TRY(launch_probe_slices(grp.stacked, grp.L, grp.magic, grp.k, lgR, R, grp.lgw, grp.slotmap, S, nC, ent,
-                                 tab, sm, slice_parts(S, nC, lgR), lgC, s, e3));
+                                 tab, sm, slice_parts(S, nC, lgR), lgC, s));
     DLSM_TRY(launch_probe_unpermute(nr, pos, sm, mask_dev + r0, lgC, s));
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }

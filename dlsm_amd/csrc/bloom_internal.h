@@ -89,7 +89,6 @@ struct LegacyJobDev {
 
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
-constexpr int kMaxSlicesE3 = 128;   // slices of a probe with 3-byte entries (4 sub-buckets each)
 constexpr uint32_t kBuildSliceCUs = 256;  // MI355X CUs: the build's slice-count target (choose_build_lgR)
 #ifndef DLSM_BUILD_CHUNK
 #define DLSM_BUILD_CHUNK 4096
@@ -156,22 +155,17 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
 // lgC: log2 keys per probe chunk (12..14); lgR: log2 stacked lines per slice
 // (7, 8 for byte-wide stacked images; 11 - lgw for packed ones, lgw < 3).
 // R: filter lines per slice (<= 256 for byte images, 2^(11-lgw) for packed).
-// e3: 3-byte entries (probe_e3_supported shapes only; the slice pass must be
-// launched with the same flag, and tab rows are 4 S + 4 u16, entries 3 bytes
-// per slot of a probe_region(C) chunk region).
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
                                   uint16_t* tab, int mode, int lgC, hipStream_t s,
-                                  uint32_t cus = 0,  // CUs the persistent grid is sized for (0: the device's)
-                                  bool e3 = false);
-bool probe_e3_supported(uint32_t n_slices, int lgC, int mode, int lgw, int lgR);
+                                  uint32_t cus = 0);  // CUs the persistent grid is sized for (0: the device's)
 // lgw 3: byte-wide stacked image (launch_stack_filters); lgw 0..2: packed
 // image (launch_pack_filters) whose member m answers in bit (slotmap >> 4m) & 7.
 // lgR: log2 of the LDS capacity in lines; R <= 2^lgR: the slice size in lines.
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k,
                                int lgR, uint32_t R, int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
-                               int parts, int lgC, hipStream_t s, bool e3 = false);
+                               int parts, int lgC, hipStream_t s);
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                   uint8_t* mask, int lgC, hipStream_t s);
 

@@ -506,11 +506,10 @@ __device__ __forceinline__ void seg_locate_win_lds(uint32_t excl, uint64_t nz, u
 // read + one list read, and the windows' chains are independent.  A segment
 // starting exactly at window u's start is counted in cw, so lane 0's flag is
 // ignored.
-template <int U, bool E3 = false>
+template <int U>
 __device__ __forceinline__ void seg_locate_set_lds(uint32_t excl, uint64_t nz, uint32_t T, uint32_t w0,
                                                    uint32_t tag, lds_u32* flg, const lds_u32* dvc,
-                                                   uint32_t (&idx)[U], bool (&ok)[U], const lds_u32* bsc,
-                                                   uint32_t (&b1)[U], uint32_t (&b2)[U], uint32_t (&b3)[U]) {
+                                                   uint32_t (&idx)[U], bool (&ok)[U]) {
   const uint32_t lane = threadIdx.x & 63;
   const bool live = (nz >> lane) & 1u;
   const uint32_t r = excl - w0;
@@ -531,22 +530,12 @@ __device__ __forceinline__ void seg_locate_set_lds(uint32_t excl, uint64_t nz, u
     const uint64_t b = __ballot(f[u] != 0u);
     const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
                                                      __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
-    const uint32_t kq = (cw + below + f[u] - 1u) & 63u;
-    const uint32_t d = dvc[kq];
+    const uint32_t d = dvc[(cw + below + f[u] - 1u) & 63u];
     const uint32_t id = w + lane + d;
     const uint32_t id0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(id), 0));
     const bool live_w = u == 0 || w < T;  // wave-uniform
     ok[u] = live_w && w + lane < T;
     idx[u] = ok[u] ? id : (live_w ? id0 : idx[0]);
-    if constexpr (E3) {  // the segment's sub-bucket bounds travel with the index
-      const uint32_t x1 = bsc[4u * kq], x2 = bsc[4u * kq + 1u], x3 = bsc[4u * kq + 2u];
-      const uint32_t y1 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x1), 0));
-      const uint32_t y2 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x2), 0));
-      const uint32_t y3 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x3), 0));
-      b1[u] = ok[u] ? x1 : (live_w ? y1 : b1[0]);
-      b2[u] = ok[u] ? x2 : (live_w ? y2 : b2[0]);
-      b3[u] = ok[u] ? x3 : (live_w ? y3 : b3[0]);
-    }
   }
 }
 
@@ -566,14 +555,9 @@ __device__ __forceinline__ void seg_locate_set_lds(uint32_t excl, uint64_t nz, u
 // NTL: the entry loads are non-temporal (the probe's 4 B/key entries are read
 // once; streaming them past the Infinity Cache keeps it for the answers the
 // unpermute pass reads next).
-// E3: 12-byte units of four 3-byte entries (E = uint4, .w unused); the table
-// rows hold 4 sub-bucket starts per slice (tb at the slice's first), and each
-// located segment also carries its sub-bucket bounds (bq: entry indices in
-// the group, as idx * 4 + j) from the wave's compacted list `bsc`.
-template <int U, uint32_t CHUNK, typename E = uint32_t, bool NTL = false, bool E3 = false>
+template <int U, uint32_t CHUNK, typename E = uint32_t, bool NTL = false>
 struct SegWalk {
-  static constexpr uint32_t kPerE = E3 ? 4u : sizeof(E) / 4;  // entries per element
-  static constexpr uint32_t kRowStep = E3 ? 4u : 1u;          // u16 from a bucket's start to its end
+  static constexpr uint32_t kPerE = sizeof(E) / 4;  // entries per element
   const uint16_t* tb;
   const uint32_t* entries;
   uint32_t rowlen, g_step, g_end;
@@ -586,25 +570,17 @@ struct SegWalk {
   uint32_t excl, dv, T;
   uint64_t nz;        // non-empty segments of the current group
   uint32_t nrow;      // prefetched table row pair of group g + g_step (this lane's chunk), packed
-  lds_u32* bsc = nullptr;  // E3: the wave's 64 compacted sub-bucket bounds (4 u32 each, LDS)
-  uint32_t nb01 = 0, nb23 = 0;  // E3: prefetched sub-bucket starts of group g + g_step, packed
 
   // The row pair (bucket start, bucket end) of this lane's chunk as one
   // packed u32, unpacked only in setup(): the load stays in flight until the
   // next group starts instead of being waited on where it is issued.
-  __device__ __forceinline__ uint32_t load_rows(uint32_t gg, uint32_t& b01, uint32_t& b23) const {
+  __device__ __forceinline__ uint32_t load_rows(uint32_t gg) const {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t c = min(min(gg, g_end) + lane, g_end - 1u);  // clamped: unconditional loads
     const uint16_t* r = tb + static_cast<uint64_t>(c) * rowlen;
-    if constexpr (E3) {  // 4-byte aligned pairs: 4 S + 4 u16 per row, 4 per slice
-      const uint32_t* r2 = reinterpret_cast<const uint32_t*>(r);
-      b01 = r2[0];
-      b23 = r2[1];
-      return (b01 & 0xffffu) | (static_cast<uint32_t>(r[kRowStep]) << 16);
-    }
-    return static_cast<uint32_t>(r[0]) | (static_cast<uint32_t>(r[kRowStep]) << 16);
+    return static_cast<uint32_t>(r[0]) | (static_cast<uint32_t>(r[1]) << 16);
   }
-  __device__ __forceinline__ void setup(uint32_t row, uint32_t b01 = 0u, uint32_t b23 = 0u) {
+  __device__ __forceinline__ void setup(uint32_t row) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t a0 = (row & 0xffffu) / kPerE, a1 = (row >> 16) / kPerE;
     const uint32_t cnt = lane < gs && g + lane < g_end ? a1 - a0 : 0u;
@@ -618,12 +594,6 @@ struct SegWalk {
       const uint32_t k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(nz >> 32),
                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(nz), 0u));
       scr[kFlags + k] = dv;
-      if constexpr (E3) {  // sub-bucket starts 1..3 as entry indices in the group
-        const uint32_t eb = lane * CHUNK * 4u;
-        bsc[4u * k] = eb + (b01 >> 16);
-        bsc[4u * k + 1u] = eb + (b23 & 0xffffu);
-        bsc[4u * k + 2u] = eb + (b23 >> 16);
-      }
     }
   }
   // The next group's rows are prefetched unconditionally (load_rows clamps
@@ -634,7 +604,7 @@ struct SegWalk {
   // returns the first row pair without waiting for it; start() hands it to
   // setup().  A caller with a prologue of its own runs it in between, so the
   // row loads' round trip overlaps it.
-  __device__ __forceinline__ bool begin(uint32_t g_first, uint32_t& row, uint32_t& b01, uint32_t& b23) {
+  __device__ __forceinline__ bool begin(uint32_t g_first, uint32_t& row) {
     g = g_first;
     if (g >= g_end) return false;
     if constexpr (U <= 2) {
@@ -642,24 +612,23 @@ struct SegWalk {
       for (int u = 0; u < kFlags / 64; u++) scr[u * 64 + (threadIdx.x & 63)] = ~0u;
       tag = 0;
     }
-    row = load_rows(g, b01, b23);
-    nrow = load_rows(g + g_step, nb01, nb23);
+    row = load_rows(g);
+    nrow = load_rows(g + g_step);
     return true;
   }
   __device__ __forceinline__ bool start(uint32_t g_first) {
-    uint32_t row, b01 = 0, b23 = 0;
-    if (!begin(g_first, row, b01, b23)) return false;
-    setup(row, b01, b23);
+    uint32_t row;
+    if (!begin(g_first, row)) return false;
+    setup(row);
     return true;
   }
   // Locate the next window set; false when the walk is done.
-  __device__ __forceinline__ bool next(uint32_t (&idx)[U], bool (&ok)[U], uint32_t& gset, uint32_t (&b1)[U],
-                                       uint32_t (&b2)[U], uint32_t (&b3)[U]) {
+  __device__ __forceinline__ bool next(uint32_t (&idx)[U], bool (&ok)[U], uint32_t& gset) {
     if (e0 >= T) {
       g += g_step;
       if (g >= g_end) return false;
-      setup(nrow, nb01, nb23);
-      nrow = load_rows(g + g_step, nb01, nb23);  // after setup: the load can refill nrow's register (no copy, no wait)
+      setup(nrow);
+      nrow = load_rows(g + g_step);  // after setup: the load can refill nrow's register (no copy, no wait)
       // Empty groups (rare): their successors' rows are loaded and waited
       // on here.  Reusing the prefetched row in this loop would put a use of
       // a just-issued load on one path into the group change, and the
@@ -668,43 +637,20 @@ struct SegWalk {
       while (e0 >= T) {
         g += g_step;
         if (g >= g_end) return false;
-        uint32_t c01 = 0, c23 = 0;
-        const uint32_t row2 = load_rows(g, c01, c23);
-        nrow = load_rows(g + g_step, nb01, nb23);
-        setup(row2, c01, c23);
+        const uint32_t row2 = load_rows(g);
+        nrow = load_rows(g + g_step);
+        setup(row2);
       }
     }
-    if constexpr (E3) {
-      static_assert(U <= 2, "E3 walks locate whole window sets");
-      seg_locate_set_lds<U, true>(excl, nz, T, e0, tag++, scr, scr + kFlags, idx, ok, bsc, b1, b2, b3);
-    } else if constexpr (U <= 2) {
-      seg_locate_set_lds<U>(excl, nz, T, e0, tag++, scr, scr + kFlags, idx, ok, bsc, b1, b2, b3);
-    } else {
+    if constexpr (U <= 2)
+      seg_locate_set_lds<U>(excl, nz, T, e0, tag++, scr, scr + kFlags, idx, ok);
+    else
       seg_locate_win_lds<U>(excl, nz, T, e0, scr, scr + kFlags, idx, ok);
-    }
     e0 += kWin * U;
     gset = g;
     return true;
   }
   __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
-    if constexpr (E3) {  // 12-byte units: three dwords per lane, 768 contiguous bytes per wave
-      const uint32_t* g3 = entries + static_cast<uint64_t>(gset) * CHUNK * 3u;
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const uint32_t* p = g3 + 3u * idx[u];
-        if constexpr (NTL) {
-          hv[u].x = __builtin_nontemporal_load(p);
-          hv[u].y = __builtin_nontemporal_load(p + 1);
-          hv[u].z = __builtin_nontemporal_load(p + 2);
-        } else {
-          hv[u].x = p[0];
-          hv[u].y = p[1];
-          hv[u].z = p[2];
-        }
-        hv[u].w = 0u;
-      }
-      return;
-    }
     const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
 #pragma unroll
     for (int u = 0; u < U; u++) {  // in-group for every lane: no select around the load
@@ -726,7 +672,6 @@ struct WinSet {
   uint32_t idx[U], g;
   E hv[U];
   bool ok[U];
-  uint32_t b1[U], b2[U], b3[U];  // E3 only (unused registers elsewhere are dropped)
 };
 
 struct NoPrologue {
@@ -737,25 +682,21 @@ struct NoPrologue {
 // run by every wave after the first row loads are issued and before they are
 // used -- their round trip overlaps it.  Every wave runs it, walk or not, so
 // it may hold workgroup barriers.
-// E3: act(hv, idx, ok, g, bq) -- the window's sub-bucket bounds too; bsc:
-// the wave's 64 uint4 of LDS for them.
-template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL = false, bool E3 = false,
-          typename Act, typename Pro = NoPrologue>
+template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL = false, typename Act,
+          typename Pro = NoPrologue>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
-                                              uint32_t* scratch, Act act, Pro pro = Pro{},
-                                              uint32_t* bscratch = nullptr) {
+                                              uint32_t* scratch, Act act, Pro pro = Pro{}) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
-  SegWalk<U, CHUNK, E, NTL, E3> w{tb, entries, rowlen, g_step, g_end, gs};
+  SegWalk<U, CHUNK, E, NTL> w{tb, entries, rowlen, g_step, g_end, gs};
   w.scr = (lds_u32*)scratch;  // generic -> LDS address space (addrspacecast)
-  w.bsc = (lds_u32*)bscratch;
-  uint32_t row0 = 0, b01 = 0, b23 = 0;
-  const bool any = w.begin(g_first, row0, b01, b23);
+  uint32_t row0 = 0;
+  const bool any = w.begin(g_first, row0);
   pro();
   if (!any) return;
-  w.setup(row0, b01, b23);
+  w.setup(row0);
   WinSet<U, CHUNK, E> A, B;
-  if (!w.next(A.idx, A.ok, A.g, A.b1, A.b2, A.b3)) return;
+  if (!w.next(A.idx, A.ok, A.g)) return;
   w.fetch(A.idx, A.g, A.hv);
   // The first set's loads land in A's registers, which the loop refills by
   // copies: left pending into the loop, the compiler's wait for them merges
@@ -765,15 +706,14 @@ __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowle
   __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
   bool haveB = false;
   if constexpr (DEPTH == 2) {
-    haveB = w.next(B.idx, B.ok, B.g, B.b1, B.b2, B.b3);
+    haveB = w.next(B.idx, B.ok, B.g);
     if (haveB) w.fetch(B.idx, B.g, B.hv);
   }
   while (true) {
     WinSet<U, CHUNK, E> N;
-    const bool more = (DEPTH == 1 || haveB) && w.next(N.idx, N.ok, N.g, N.b1, N.b2, N.b3);
+    const bool more = (DEPTH == 1 || haveB) && w.next(N.idx, N.ok, N.g);
     if (more) w.fetch(N.idx, N.g, N.hv);
-    if constexpr (E3) act(A.hv, A.idx, A.ok, A.g, A.b1, A.b2, A.b3);
-    else act(A.hv, A.idx, A.ok, A.g);
+    act(A.hv, A.idx, A.ok, A.g);
     if constexpr (DEPTH == 1) {
       if (!more) break;
       A = N;
@@ -809,42 +749,6 @@ __device__ __forceinline__ void store_chunk_u32(uint32_t* g, const uint32_t* lds
     store16<NTS>(reinterpret_cast<uint4*>(g) + v, reinterpret_cast<const uint4*>(lds)[v]);
   for (uint32_t i = nv * 4u + threadIdx.x; i < n; i += NT) g[i] = lds[i];
 }
-// n (a multiple of 4) 24-bit entries staged as u32 in LDS, stored packed 4
-// to a 12-byte unit: each lane packs 16 entries into three 16-byte stores
-// (48 contiguous bytes per lane), the last < 16 entries as dwords.
-template <int NT, bool NTS = false>
-__device__ __forceinline__ void store_chunk_e3(uint32_t* g, const uint32_t* lds, uint32_t n) {
-  auto pack = [](const uint32_t* e, uint32_t* w) {  // 4 entries -> 3 dwords
-    w[0] = e[0] | (e[1] << 24);
-    w[1] = (e[1] >> 8) | (e[2] << 16);
-    w[2] = (e[2] >> 16) | (e[3] << 8);
-  };
-  const uint32_t n16 = n / 16u;
-  for (uint32_t v = threadIdx.x; v < n16; v += NT) {
-    uint32_t e[16], w[12];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const uint4 x = reinterpret_cast<const uint4*>(lds)[4u * v + q];
-      e[4 * q] = x.x; e[4 * q + 1] = x.y; e[4 * q + 2] = x.z; e[4 * q + 3] = x.w;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) pack(e + 4 * q, w + 3 * q);
-#pragma unroll
-    for (int q = 0; q < 3; q++)
-      store16<NTS>(reinterpret_cast<uint4*>(g + 12u * v) + q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
-  }
-  const uint32_t nu = n / 4u;
-  for (uint32_t u = 4u * n16 + threadIdx.x; u < nu; u += NT) {
-    const uint4 x = reinterpret_cast<const uint4*>(lds)[u];
-    const uint32_t e[4] = {x.x, x.y, x.z, x.w};
-    uint32_t w[3];
-    pack(e, w);
-    g[3u * u] = w[0];
-    g[3u * u + 1] = w[1];
-    g[3u * u + 2] = w[2];
-  }
-}
-
 template <int NT, bool NTS = false>
 __device__ __forceinline__ void store_chunk_u16(uint16_t* g, const uint16_t* lds, uint32_t n) {
   const uint32_t nv = n / 8u;
@@ -1269,23 +1173,6 @@ __device__ __forceinline__ uint32_t probe_entry_off(uint32_t e) {
   return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
 }
 
-// 3-byte probe entry (E3): bits [0, 9) = h's first bit position, [9, 18) =
-// the low 9 bits of delta = rotr(h, 17) (h bits [17, 26)), [18, 24) = the
-// key's line inside its sub-slice (< 64); the sub-slice (quarter of the
-// slice) is the entry's sub-bucket, known from its place in the bucket.
-// Bucket padding is 0 (probed like any entry; its answer byte is never read).
-__device__ __forceinline__ uint32_t probe_entry3(uint32_t h, uint32_t off6) {
-  return (h & 0x1ffu) | (((h >> 17) & 0x1ffu) << 9) | (off6 << 18);
-}
-
-// Position of a ranked key in its chunk's bucketed order: E3 ranks carry the
-// sub-slice in bits 14-15.
-template <bool E3>
-__device__ __forceinline__ uint32_t bucket_pos(const uint32_t* hist, uint32_t sl, uint32_t rk) {
-  if constexpr (E3) return hist[4 * sl + (rk >> 14)] + (rk & 0x3fffu);
-  return hist[sl] + rk;
-}
-
 // f(b) for every bucket b < n (n <= kMaxSlices + 1): one bucket per thread
 // when the workgroup has enough threads.  A strided loop's per-lane trip
 // count is a loop invariant the persistent partition spilled to scratch, and
@@ -1299,15 +1186,6 @@ __device__ __forceinline__ void for_buckets(uint32_t n, F f) {
     for (uint32_t b = threadIdx.x; b < n; b += NT) f(b);
   }
 }
-// The same over up to NB buckets.
-template <int NT, uint32_t NB, typename F>
-__device__ __forceinline__ void for_buckets_n(uint32_t n, F f) {
-  if constexpr (NT >= static_cast<int>(NB)) {
-    if (threadIdx.x < n) f(threadIdx.x);
-  } else {
-    for (uint32_t b = threadIdx.x; b < n; b += NT) f(b);
-  }
-}
 
 // Pass 1: hash each lookup once and bucket it by slice inside its chunk.
 // entries[chunk region of probe_region(C) u32] = packed entries (probe_entry)
@@ -1316,11 +1194,7 @@ __device__ __forceinline__ void for_buckets_n(uint32_t n, F f) {
 // key i went.  NT threads per chunk of C keys (C/NT keys per thread).
 // NTS: non-temporal stores of the intermediates (default); plain stores
 // leave them in the Infinity Cache for a round-sized batch to re-read.
-// E3: 3-byte entries (probe_entry3) -- each slice's bucket is ordered by the
-// quarter of the slice (sub-slice of Rq = ceil(R / 4) lines) its key's line
-// falls in, the table row holds every sub-bucket's start (4 S + 4 u16, the
-// row padded to 8 bytes), and the entries are stored 4 to a 12-byte unit.
-template <int MODE, int NT, int C, int H = 1, bool NTS = true, bool E3 = false>
+template <int MODE, int NT, int C, int H = 1, bool NTS = true>
 __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, uint32_t R, uint32_t rmagic, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
@@ -1343,17 +1217,11 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   __shared__ __attribute__((aligned(16))) uint16_t rk[C];  // rank in bucket, then position
   __shared__ uint8_t sb[C];                                // slice (S <= 256)
   __shared__ uint32_t park[H > 1 ? (H - 1) * CH : 1];      // entries of units 0..H-2
-  // E3: 4 sub-buckets per slice (S <= kMaxSlicesE3), ranks carry the
-  // sub-slice in their bits 14-15 (C <= 8192: ranks < 2^13)
-  static_assert(!E3 || C <= 8192, "E3 ranks");
-  constexpr uint32_t NB = E3 ? 4 * kMaxSlicesE3 + 1 : kMaxSlices + 1;
-  __shared__ uint32_t hist[NB];
+  __shared__ uint32_t hist[kMaxSlices + 1];
   __shared__ uint8_t npad[kMaxSlices + 1];
   __shared__ uint32_t wsum[NT / 64];
   const int tid = threadIdx.x;
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
-  const uint32_t Rq = (R + 3u) >> 2;  // E3 sub-slice lines
-  const uint32_t SB = E3 ? 4 * S : S;  // buckets
   auto chunk_keys = [&](uint32_t cc) {
     const uint64_t left = kd.n - static_cast<uint64_t>(cc) * C;
     return left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
@@ -1380,7 +1248,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
     const uint64_t first = static_cast<uint64_t>(c) * C;
     const uint32_t nk = chunk_keys(c);
-    for_buckets_n<NT, NB>(SB + 1, [&](uint32_t b) { hist[b] = 0; });
+    for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
     uint32_t h[PER];
 #pragma unroll
     for (int u = 0; u < H; u++) {
@@ -1408,42 +1276,29 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
           uint32_t off;  // slices of R lines (not a power of two when balanced over the CUs)
           const uint32_t sl = fastdivmod(line, R, rmagic, &off);
           sb[i] = static_cast<uint8_t>(sl);
-          if constexpr (E3) {
-            const uint32_t q = (off >= Rq) + (off >= 2 * Rq) + (off >= 3 * Rq);
-            rk[i] = static_cast<uint16_t>(atomicAdd(&hist[4 * sl + q], 1u) | (q << 14));
-            h[r] = probe_entry3(h[r], off - q * Rq);
-          } else {
-            rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
-            h[r] = probe_entry(h[r], off);
-          }
+          rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+          h[r] = probe_entry(h[r], off);
           if (u + 1 < H) park[i] = h[r];
         }
       }
     }
     __syncthreads();
-    for_buckets<NT>(S, [&](uint32_t b) {  // pad every (slice) bucket to whole units of 4 entries
-      if constexpr (E3) {  // the pad goes after the slice's last sub-bucket
-        const uint32_t pad = (0u - (hist[4 * b] + hist[4 * b + 1] + hist[4 * b + 2] + hist[4 * b + 3])) & 3u;
-        npad[b] = static_cast<uint8_t>(pad);
-        hist[4 * b + 3] += pad;
-      } else {
-        const uint32_t pad = (0u - hist[b]) & 3u;
-        npad[b] = static_cast<uint8_t>(pad);
-        hist[b] += pad;
-      }
+    for_buckets<NT>(S, [&](uint32_t b) {  // pad every bucket to whole 16-byte units
+      const uint32_t pad = (0u - hist[b]) & 3u;
+      npad[b] = static_cast<uint8_t>(pad);
+      hist[b] += pad;
     });
     __syncthreads();
-    const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(SB + 1), wsum);
-    const uint32_t rowlen = E3 ? SB + 4 : S + 1;  // E3 rows padded to 8 bytes
-    for_buckets_n<NT, NB>(SB + 1, [&](uint32_t b) {  // one row per chunk
-      tab[static_cast<uint64_t>(c) * rowlen + b] = static_cast<uint16_t>(hist[b]);
+    const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
+    for_buckets<NT>(S + 1, [&](uint32_t b) {  // one row per chunk
+      tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
     });
     for_buckets<NT>(S, [&](uint32_t b) {
-      const uint32_t end = hist[E3 ? 4 * b + 4 : b + 1];
+      const uint32_t end = hist[b + 1];
       const uint32_t np = npad[b];
-      if (np > 0) stage[end - 1] = E3 ? 0u : kProbePadEntry;
-      if (np > 1) stage[end - 2] = E3 ? 0u : kProbePadEntry;
-      if (np > 2) stage[end - 3] = E3 ? 0u : kProbePadEntry;
+      if (np > 0) stage[end - 1] = kProbePadEntry;
+      if (np > 1) stage[end - 2] = kProbePadEntry;
+      if (np > 2) stage[end - 3] = kProbePadEntry;
     });
     const uint32_t nkl = unit_keys(nk, H - 1);
 #pragma unroll
@@ -1451,7 +1306,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
       const uint32_t il = r * NT + tid;
       const uint32_t i = static_cast<uint32_t>(H - 1) * CH + il;
       if (il < nkl) {
-        const uint32_t p = bucket_pos<E3>(hist, sb[i], rk[i]);
+        const uint32_t p = hist[sb[i]] + rk[i];
         stage[p] = h[r];
         rk[i] = static_cast<uint16_t>(p);
       }
@@ -1459,7 +1314,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     if constexpr (H > 1) {  // the parked units
       const uint32_t np = min(nk, static_cast<uint32_t>((H - 1) * CH));
       for (uint32_t i = tid; i < np; i += NT) {
-        const uint32_t p = bucket_pos<E3>(hist, sb[i], rk[i]);
+        const uint32_t p = hist[sb[i]] + rk[i];
         stage[p] = park[i];
         rk[i] = static_cast<uint16_t>(p);
       }
@@ -1470,10 +1325,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     // every wait is a full vmcnt(0) that would also wait for their acks.
     if constexpr (kPipe) __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
     // coalesced 16-byte stores of the bucketed entries and of the positions
-    if constexpr (E3)
-      store_chunk_e3<NT, NTS>(entries + static_cast<uint64_t>(c) * (CR / 4) * 3, stage, total);
-    else
-      store_chunk_u32<NT, NTS>(entries + static_cast<uint64_t>(c) * CR, stage, total);
+    store_chunk_u32<NT, NTS>(entries + static_cast<uint64_t>(c) * CR, stage, total);
     store_chunk_u16<NT, NTS>(pos + first, rk, nk);
     __syncthreads();  // LDS reused by the next chunk
   }
@@ -1505,9 +1357,7 @@ __device__ __forceinline__ uint32_t packed_answer(uint32_t acc, uint32_t slotmap
 // LGW 0..2: packed image of a group of 1, 2 or 3-4 filters (a W-bit field per
 // bit position: 8 / 4 / 2 times the lines per slice), whose member m answers
 // in bit (slotmap >> 4m) & 7.
-// E3 (byte-wide images, LGW 3): 3-byte entries in 12-byte units, sub-bucketed
-// by quarter slice (probe_partition_kernel E3).
-template <int LGR, int LGW, int K, int NT, int C, bool E3 = false>
+template <int LGR, int LGW, int K, int NT, int C>
 __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     const uint8_t* __restrict__ stacked, uint32_t L, uint32_t Rs, uint32_t slotmap, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
@@ -1521,10 +1371,8 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   // 4 waves per SIMD, so each carries two windows (measured best per shape)
   constexpr int U = LGR + LGW >= 11 ? kProbeWalkU8 : kProbeWalkU;
   constexpr int NW = NT / 64;
-  static_assert(!E3 || LGW == 3, "3-byte entries address byte-wide images");
   __shared__ __attribute__((aligned(16))) uint8_t sl[R * LB];
   __shared__ uint32_t walk_scr[NW * kWalkScratch];
-  __shared__ uint32_t walk_b3[E3 ? NW * 64 * 4 : 1];  // E3: each wave's compacted sub-bucket bounds
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
@@ -1542,10 +1390,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t nw = nl * (LB / 16);
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
-  // chunk-major rows of S+1 u16 (E3: 4 S + 4, a slice's 4 sub-bucket starts)
-  const uint16_t* tb = tab + (E3 ? 4 * s : s);
-  const uint32_t rowlen = E3 ? 4 * S + 4 : S + 1;
-  const uint32_t Rq = (Rs + 3u) >> 2;  // E3 sub-slice lines
+  const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
   constexpr uint32_t CRU = probe_region(C) / 4;  // chunk region stride in 16-byte units
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
@@ -1607,58 +1452,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
 #pragma unroll
         for (int u = 0; u < U; u++) gmask[idx[u]] = ans[u];
   };
-  // E3: four 24-bit entries per 12-byte unit; entry j of unit idx is entry
-  // idx * 4 + j of the group, its sub-slice the count of the segment's
-  // sub-bucket starts (bq) at or below it.
-  auto probe_set3 = [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g,
-                        const uint32_t (&b1)[U], const uint32_t (&b2)[U], const uint32_t (&b3)[U]) {
-    uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
-    uint32_t ans[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t e4[4] = {hv[u].x & 0xffffffu, (hv[u].x >> 24) | ((hv[u].y & 0xffffu) << 8),
-                              (hv[u].y >> 16) | ((hv[u].z & 0xffu) << 16), hv[u].z >> 8};
-      uint32_t a = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        uint32_t x = e4[j];
-        const uint32_t ei = idx[u] * 4u + static_cast<uint32_t>(j);
-        const uint32_t q = (ei >= b1[u]) + (ei >= b2[u]) + (ei >= b3[u]);
-        const uint32_t base = (q * Rq + (x >> 18)) << 9;  // sub-slice line * 512 stacked bytes
-        const uint32_t delta = x >> 9;                    // low 9 bits of rotr(h, 17)
-        uint32_t acc = 0xffu;
-        if constexpr (K > 0) {
-#pragma unroll
-          for (int t = 0; t < K; t++) {
-            acc &= sl[base | (x & 511u)];
-            x += delta;
-          }
-        } else {
-          for (int t = 0; t < k; t++) {
-            acc &= sl[base | (x & 511u)];
-            x += delta;
-          }
-        }
-        a |= acc << (8 * j);
-      }
-      ans[u] = a;
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) gmask[idx[u]] = ans[u];  // unconditional: see probe_set
-  };
-  if constexpr (E3) {
-    auto slice_to_lds = [&] {
-      uint4 t[V];
-#pragma unroll
-      for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
-#pragma unroll
-      for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
-      __syncthreads();
-    };
-    walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0, true>(
-        tb, rowlen, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set3,
-        slice_to_lds, walk_b3 + wv * 256);
-  } else if constexpr (LGW == 3) {
+  if constexpr (LGW == 3) {
     // byte-wide images: the slice load runs as the walk's prologue, after the
     // walk's first table-row loads are issued (one round trip fewer before
     // the first entries load: small batches)
@@ -1671,7 +1465,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
       __syncthreads();
     };
     walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
-        tb, rowlen, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
+        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
         slice_to_lds);
   } else {
     // packed images: the same load in front of the walk (as the walk's
@@ -1685,7 +1479,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     }
     __syncthreads();
     walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
-        tb, rowlen, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set);
+        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set);
   }
 }
 
@@ -2175,7 +1969,7 @@ static uint32_t device_cus() {
 template <int C, int NT, int H = 1>
 static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                      uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                     uint16_t* tab, int mode, hipStream_t s, uint32_t cus, bool e3) {
+                                     uint16_t* tab, int mode, hipStream_t s, uint32_t cus) {
   const uint32_t nC = static_cast<uint32_t>((keys.n + C - 1) / C);
   if (nC == 0) return hipSuccess;
   // persistent: a few resident workgroups per CU loop over the chunks
@@ -2191,18 +1985,6 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, u
     const char* e = getenv("DLSM_PROBE_PLAIN_STORES");
     return e && atoi(e) != 0;
   }();
-  if constexpr (C <= 8192) {
-    if (e3 && n_slices <= kMaxSlicesE3 && (mode == KM_K20 || mode == KM_K28)) {
-      if (mode == KM_K20)
-        probe_partition_kernel<KM_K20, NT, C, H, true, true><<<g, NT, 0, s>>>(
-            keys, L, magic, R, fastmod_magic(R), n_slices, nC, entries, pos, tab);
-      else
-        probe_partition_kernel<KM_K28, NT, C, H, true, true><<<g, NT, 0, s>>>(
-            keys, L, magic, R, fastmod_magic(R), n_slices, nC, entries, pos, tab);
-      return hipGetLastError();
-    }
-  }
-  if (e3) return hipErrorInvalidValue;  // the caller asked for a shape E3 does not cover
   if (mode == KM_HASH)
     probe_partition_kernel<KM_HASH, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
                                                            entries, pos, tab);
@@ -2223,45 +2005,28 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, u
 
 hipError_t launch_probe_partition(KeyDesc keys, uint32_t L, uint32_t magic, uint32_t R,
                                   uint32_t n_slices, uint32_t* entries, uint16_t* pos,
-                                  uint16_t* tab, int mode, int lgC, hipStream_t s, uint32_t cus, bool e3) {
+                                  uint16_t* tab, int mode, int lgC, hipStream_t s, uint32_t cus) {
   switch (lgC) {
-    case 12: return probe_partition_as<4096, 512>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus, e3);
+    case 12: return probe_partition_as<4096, 512>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #if DLSM_PROBE_P13_HALF
     // 512-thread workgroups of two 4,096-key units (two resident per CU)
-    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus, e3);
+    case 13: return probe_partition_as<8192, 512, 2>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #else
-    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus, e3);
+    case 13: return probe_partition_as<8192, 1024>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
 #endif
     // 16,384-key chunks bucketed as two 8,192-key units (DLSM_PROBE_UNITS14)
-    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus, e3);
+    case 14: return probe_partition_as<16384, 1024, DLSM_PROBE_UNITS14>(keys, L, magic, R, n_slices, entries, pos, tab, mode, s, cus);
     default: return hipErrorInvalidValue;
   }
-}
-
-bool probe_e3_supported(uint32_t n_slices, int lgC, int mode, int lgw, int lgR) {
-  return n_slices <= static_cast<uint32_t>(kMaxSlicesE3) && lgC <= 13 && (mode == KM_K20 || mode == KM_K28) &&
-         lgw == 3 && lgR <= 8;
 }
 
 template <int LGR, int LGW, int C>
 static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t R, uint32_t slotmap, int k,
                                   uint32_t n_slices, uint32_t n_chunks, const uint32_t* entries,
-                                  const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s, bool e3) {
+                                  const uint16_t* tab, uint8_t* smask, int parts, hipStream_t s) {
   const uint8_t* st = reinterpret_cast<const uint8_t*>(stacked);
   constexpr int NT = DLSM_PROBE_NT;
   if (R == 0 || R > (1u << LGR)) return hipErrorInvalidValue;
-  if constexpr (LGW == 3 && C <= 8192) {
-    if (e3) {
-      if (k == 6)
-        probe_slice_kernel<LGR, LGW, 6, NT, C, true><<<n_slices * parts, NT, 0, s>>>(
-            st, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
-      else
-        probe_slice_kernel<LGR, LGW, 0, NT, C, true><<<n_slices * parts, NT, 0, s>>>(
-            st, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
-      return hipGetLastError();
-    }
-  }
-  if (e3) return hipErrorInvalidValue;
   if (k == 6)  // bits_per_key 10 (ChooseNumProbes)
     probe_slice_kernel<LGR, LGW, 6, NT, C><<<n_slices * parts, NT, 0, s>>>(
         st, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts);
@@ -2274,11 +2039,11 @@ static hipError_t probe_slices_as(const uint64_t* stacked, uint32_t L, uint32_t 
 hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t magic, int k, int lgR, uint32_t R,
                                int lgw, uint32_t slotmap, uint32_t n_slices, uint32_t n_chunks,
                                const uint32_t* entries, const uint16_t* tab, uint8_t* smask, int parts,
-                               int lgC, hipStream_t s, bool e3) {
+                               int lgC, hipStream_t s) {
   (void)magic;  // the partition already reduced every hash to its slice and line
   if (n_chunks == 0) return hipSuccess;
 #define DLSM_SLICES(LG, LW, CC) \
-  return probe_slices_as<LG, LW, CC>(stacked, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts, s, e3)
+  return probe_slices_as<LG, LW, CC>(stacked, L, R, slotmap, k, n_slices, n_chunks, entries, tab, smask, parts, s)
 #define DLSM_SLICES_C(LG, LW)                  \
   do {                                         \
     if (lgC == 12) DLSM_SLICES(LG, LW, 4096);  \

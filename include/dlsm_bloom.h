@@ -163,12 +163,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             count then takes a slower per-slice re-hash fallback)
  *   DLSM_OPT_PROBE_ROUND_SERIAL 1: probe rounds run one after another on the context
  *                             stream (one buffer set) instead of pipelined over two
- *                             streams (default 0, or $DLSM_PROBE_SERIAL)
- *   DLSM_OPT_PROBE_ENTRY_BYTES bytes per bucketed lookup entry of the sliced probe:
- *                             3 (sub-slice-ordered buckets, 12-byte units) where the
- *                             shape allows it (one byte-wide stacked image of <= 128
- *                             slices, chunks of <= 8,192 keys), else 4; or 4 always
- *                             (default 3, or $DLSM_PROBE_ENTRY_BYTES) */
+ *                             streams (default 0, or $DLSM_PROBE_SERIAL) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
@@ -176,7 +171,6 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_PROBE_SLICE_LG 4
 #define DLSM_OPT_BUILD_EXACT 5
 #define DLSM_OPT_PROBE_ROUND_SERIAL 6
-#define DLSM_OPT_PROBE_ENTRY_BYTES 7
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 /* The current value of an option (so a caller can restore it). */
 int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);
