@@ -36,3 +36,16 @@ def test_traffic_summary_matches_default_config():
 
 def test_host_cores_positive():
     assert _bench().host_cores() >= 1
+
+
+def test_step_roofline_and_pass_timing_note():
+    """The whole step's algorithmic rate beside the dominant pass's own, and
+    the note saying how the pass times were taken (sampled steps, run alone
+    when the build overlaps the probe)."""
+    b = _bench()
+    step_bytes = 100_000_000 * 21 + 16_000_552 + 16 * 1_600_000 * 20 + 16 * 2_000_069
+    r = b.step_roofline(step_bytes, 0.82e-3)
+    assert abs(r["step_alg_GBs"] - step_bytes / 0.82e-3 / 1e9) < 0.1
+    assert abs(r["step_frac"] - r["step_alg_GBs"] / b.HBM_PEAK_GBS) < 1e-4
+    assert "alone" in b.pass_timing_note(True, 12)["pass_timing"]
+    assert "every 12-th" in b.pass_timing_note(False, 12)["pass_timing"]
