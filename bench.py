@@ -219,8 +219,13 @@ def main():
 
         dwork, _keep = MG.device_work(ctx, ctx_b, inp)
         if dist:
+            # warm-up first, then a barrier right before the timed steps
+            if args.warmup:
+                MG.native_run([dwork], args.warmup, 0, bpk, event_every=args.warmup)
             dist.barrier()
-        elapsed, passes = MG.native_run([dwork], args.steps, args.warmup, bpk)
+            elapsed, passes = MG.native_run([dwork], args.steps, 0, bpk)
+        else:
+            elapsed, passes = MG.native_run([dwork], args.steps, args.warmup, bpk)
         elapsed = SH.max_over_ranks(elapsed, dist, dev)
         build_ms = float(np.mean([b for b, _ in passes]))
         probe_ms = float(np.mean([p for _, p in passes]))
