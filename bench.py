@@ -107,6 +107,8 @@ def main():
                          "(the default for --gpus N > 1; at N = 1 the Python loop is the default)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-legacy", action="store_true",
+                    help="skip the legacy-format leg (util/bloom.cc CreateFilter over the same tables)")
     args = ap.parse_args()
 
     # launch shape: torchrun (WORLD_SIZE set) = one process per GPU, and its
@@ -410,10 +412,17 @@ def main():
         result["other_step_shape"] = other_shape_rate(args, ctx, stream, tables, outs, lens, fs, qk, mask, bpk,
                                                       local, elapsed / args.steps, overlap)
 
+    # ---- legacy FilterPolicy format over the same tables (config 2's
+    # "bit-exact vs util/bloom.cc"), N=1: recorded beside `value` ----
+    legacy_out = None
+    if world == 1 and tables and not args.no_legacy:
+        result["legacy"], legacy_out = legacy_leg(ctx, stream, tables, bpk)
+
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if world == 1 and rank == 0 and not args.no_cpu:
         filters = [f for f in inp.filters]
-        result["cpu_baseline"] = cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk)
+        result["cpu_baseline"] = cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk,
+                                              legacy_out=legacy_out)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -622,7 +631,7 @@ def host_cores() -> int:
     return max(1, n)
 
 
-def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
+def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk, legacy_out=None):
     """The CPU path timed on this box's host cores on a bounded sample of the
     bench workload, at T = 1 and T = all cores: the reference's own code
     (oracle/_ref/libref.so, built in place from /root/reference, when it
@@ -648,6 +657,9 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
     allc = oracle.timed_cpu_baseline(kind, h_tabs, N, h_filters, h_q, nq, bpk, threads)
     parity = (all(gpu_filters[s] == allc["built"][s] for s in range(T))
               and bool(np.array_equal(gpu_mask, allc["mask"])) and one["built"][0] == gpu_filters[0])
+    legacy_parity = None
+    if legacy_out is not None:
+        legacy_parity = all(legacy_out[s] == allc["legacy"][s] for s in range(len(allc["legacy"])))
     sample_keys = T * N + nq
 
     def rates(r, nt, nqq, nth):
@@ -670,10 +682,60 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk):
         "host_cores_available": cores,
         "gpu_output_matches_" + kind: bool(parity),
     }
+    if legacy_parity is not None:
+        out["gpu_legacy_output_matches_" + kind] = bool(legacy_parity)
     if kind == "reference":
         out["sample"] += ("; util/bloom_impl.h AddHash / HashMayMatch + util/hash.cc + util/bloom.cc "
                           "compiled from the reference (full_filter_block.cc's bookkeeping restated)")
     return out
+
+
+def legacy_leg(ctx, stream, tables, bpk, reps=20, direct_reps=3):
+    """util/bloom.cc CreateFilter (the legacy FilterPolicy format) for the same
+    tables in one device-resident batch (dlsm_bloom_legacy_build_dev): the
+    LDS-tiled path (auto) timed with HIP events over `reps` calls on the
+    context's stream, the direct global-atomic path (path 1) beside it.
+    Algorithmic bytes: 20 B key read + the filter written once (bits/8 + 1 B,
+    1.25 B/key at 10 bits/key).  Returns (record, host filters of the tiled
+    path)."""
+    import torch
+
+    import dlsm_amd
+
+    dev = tables[0].data.device
+    outs = [torch.zeros(dlsm_amd.legacy_size(t.n, bpk) + 16, dtype=torch.uint8, device=dev) for t in tables]
+    lens = torch.zeros(len(tables), dtype=torch.uint64, device=dev)
+
+    def timed(path, n):
+        ctx.set_path(path)
+        try:
+            for _ in range(2):
+                ctx.legacy_build_dev(tables, outs, lens, bpk)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(n):
+                ctx.legacy_build_dev(tables, outs, lens, bpk)
+            e1.record(stream)
+            stream.synchronize()
+        finally:
+            ctx.set_path(0)
+        return e0.elapsed_time(e1) / n
+
+    direct_ms = timed(1, direct_reps)
+    direct = [o[: int(n)].cpu().numpy().tobytes() for o, n in zip(outs, lens.cpu().numpy())]
+    ms = timed(0, reps)
+    L = lens.cpu().numpy()
+    got = [o[: int(n)].cpu().numpy().tobytes() for o, n in zip(outs, L)]
+    nk = sum(t.n for t in tables)
+    alg = nk * 20 + int(L.sum())
+    gbs = alg / (ms * 1e-3) / 1e9
+    rec = {"ms": round(ms, 4), "mkeys_s": round(nk / ms / 1e3, 1), "alg_GBs": round(gbs, 1),
+           "alg_bytes_per_key": round(alg / nk, 3), "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "kernels": "legacy_partition_kernel + legacy_slice_kernel (tile-bucketed u16 positions, LDS ds_or)",
+           "direct_path_ms": round(direct_ms, 4), "direct_path_mkeys_s": round(nk / direct_ms / 1e3, 1),
+           "tiled_equals_direct": got == direct,
+           "note": "util/bloom.cc CreateFilter for the same tables (config 2's format), not `value`"}
+    return rec, got
 
 
 def pass_timing_note(overlapped: bool, every: int) -> dict:

@@ -71,6 +71,8 @@ SIGNATURES = [
     ("dlsm_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("dlsm_ctx_create", C.c_int, [C.c_int, C.POINTER(_VP)]),
     ("dlsm_ctx_destroy", C.c_int, [_VP]),
+    ("dlsm_thread_ctx", C.c_int, [C.POINTER(_VP)]),
+    ("dlsm_thread_ctx_bind", C.c_int, [_VP]),
     ("dlsm_ctx_set_stream", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_stream", _VP, [_VP]),
     ("dlsm_ctx_sync", C.c_int, [_VP]),
@@ -132,6 +134,7 @@ SIGNATURES = [
     ("dlsm_batcher_destroy", C.c_int, [_VP]),
     ("dlsm_batcher_full_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, _U64P]),
     ("dlsm_batcher_full_build_hashed", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, _U64P]),
+    ("dlsm_batcher_submit", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_batcher_stats", C.c_int, [_VP, _U64P, _U64P, _U64P]),
     ("dlsm_multi_device_run", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
                                        C.POINTER(C.c_double), C.POINTER(C.c_float)]),

@@ -13,8 +13,9 @@
 // executor's batch is in flight the next gathers the calls that arrive
 // meanwhile, so batching adapts to the arrival rate.  Results are those of
 // the per-table call (same kernels, same bytes).
-#include <hip/hip_runtime.h>
-
+// Host code only (no HIP calls of its own: every device call goes through
+// the C ABI), so tests/cpp/batcher_cpu_test.cc compiles it with g++ against
+// a stubbed ABI under ThreadSanitizer.
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -29,7 +30,7 @@ namespace {
 struct Request {
   const dlsm_build_job* job;
   int bpk;
-  bool hashed;
+  int flags;  // DLSM_BATCH_HASHED | DLSM_BATCH_EXACT
   uint64_t out_len = 0;
   int status = DLSM_OK;
   bool done = false;
@@ -47,6 +48,15 @@ struct dlsm_batcher {
   std::vector<dlsm_ctx*> ctxs;
   uint64_t batches = 0, jobs = 0, max_batch = 0;
 
+  static int build(dlsm_ctx* ctx, const dlsm_build_job* jv, int n, int bpk, int flags, uint64_t* lens) {
+    // the executor's context counts the line number exactly first when the
+    // batch's builders saw repeated keys (their filters would otherwise take
+    // the slice pass's re-hash fallback for a lowered line count)
+    dlsm_ctx_set_option(ctx, DLSM_OPT_BUILD_EXACT, (flags & DLSM_BATCH_EXACT) ? 1 : 0);
+    return (flags & DLSM_BATCH_HASHED) ? dlsm_bloom_full_build_hashed(ctx, jv, n, bpk, lens)
+                                       : dlsm_bloom_full_build(ctx, jv, n, bpk, lens);
+  }
+
   void run(dlsm_ctx* ctx) {
     std::vector<Request*> batch;
     std::vector<dlsm_build_job> jv;
@@ -55,14 +65,21 @@ struct dlsm_batcher {
       std::unique_lock<std::mutex> lk(m);
       cv_work.wait(lk, [&] { return stop || !q.empty(); });
       if (q.empty()) return;  // stop, nothing left
-      if (window_us && q.size() < max_jobs && !stop)
+      if (window_us && q.size() < max_jobs && !stop) {
         cv_work.wait_for(lk, std::chrono::microseconds(window_us), [&] { return stop || q.size() >= max_jobs; });
-      // every queued job with the front's (bits_per_key, hashed): one call
+        // another executor may have taken every queued job while this one
+        // waited in its window
+        if (q.empty()) {
+          if (stop) return;
+          continue;
+        }
+      }
+      // every queued job with the front's (bits_per_key, flags): one call
       batch.clear();
       const int bpk = q.front()->bpk;
-      const bool hashed = q.front()->hashed;
+      const int flags = q.front()->flags;
       for (auto it = q.begin(); it != q.end() && batch.size() < max_jobs;) {
-        if ((*it)->bpk == bpk && (*it)->hashed == hashed) {
+        if ((*it)->bpk == bpk && (*it)->flags == flags) {
           batch.push_back(*it);
           it = q.erase(it);
         } else {
@@ -74,18 +91,27 @@ struct dlsm_batcher {
       jobs += batch.size();
       if (batch.size() > max_batch) max_batch = batch.size();
       lk.unlock();
-      jv.resize(batch.size());
-      lens.assign(batch.size(), 0);
-      for (size_t i = 0; i < batch.size(); i++) jv[i] = *batch[i]->job;
       const int n = static_cast<int>(batch.size());
-      const int st = hashed ? dlsm_bloom_full_build_hashed(ctx, jv.data(), n, bpk, lens.data())
-                            : dlsm_bloom_full_build(ctx, jv.data(), n, bpk, lens.data());
-      lk.lock();
-      for (size_t i = 0; i < batch.size(); i++) {
-        Request* r = batch[i];
-        r->out_len = lens[i];
+      jv.resize(n);
+      lens.assign(n, 0);
+      std::vector<int> status(n, DLSM_OK);
+      for (int i = 0; i < n; i++) jv[i] = *batch[i]->job;
+      const int st = build(ctx, jv.data(), n, bpk, flags, lens.data());
+      if (st == DLSM_OK || st == DLSM_E_CAPACITY) {
         // a batch's only per-job failure is a too-small slot (its length 0)
-        r->status = st == DLSM_OK ? DLSM_OK : (st == DLSM_E_CAPACITY ? (lens[i] ? DLSM_OK : DLSM_E_CAPACITY) : st);
+        for (int i = 0; i < n; i++) status[i] = lens[i] ? DLSM_OK : (st == DLSM_OK ? DLSM_OK : DLSM_E_CAPACITY);
+      } else if (n == 1) {
+        status[0] = st;
+      } else {
+        // one job's invalid keyset (or a device error) failed the batched call:
+        // run the jobs one at a time so every caller gets its own status
+        for (int i = 0; i < n; i++) status[i] = build(ctx, &jv[i], 1, bpk, flags, &lens[i]);
+      }
+      lk.lock();
+      for (int i = 0; i < n; i++) {
+        Request* r = batch[i];
+        r->out_len = status[i] == DLSM_OK ? lens[i] : 0;
+        r->status = status[i];
         r->done = true;
       }
       cv_done.notify_all();
@@ -131,9 +157,9 @@ int dlsm_batcher_destroy(dlsm_batcher* b) {
   return DLSM_OK;
 }
 
-static int submit(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, bool hashed, uint64_t* out_len) {
-  if (!b || !job || !out_len) return DLSM_E_ARG;
-  Request r{job, bits_per_key, hashed};
+int dlsm_batcher_submit(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, int flags, uint64_t* out_len) {
+  if (!b || !job || !out_len || (flags & ~(DLSM_BATCH_HASHED | DLSM_BATCH_EXACT))) return DLSM_E_ARG;
+  Request r{job, bits_per_key, flags};
   std::unique_lock<std::mutex> lk(b->m);
   if (b->stop) return DLSM_E_ARG;
   b->q.push_back(&r);
@@ -144,12 +170,12 @@ static int submit(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, 
 }
 
 int dlsm_batcher_full_build(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, uint64_t* out_len) {
-  return submit(b, job, bits_per_key, false, out_len);
+  return dlsm_batcher_submit(b, job, bits_per_key, 0, out_len);
 }
 
 int dlsm_batcher_full_build_hashed(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key,
                                    uint64_t* out_len) {
-  return submit(b, job, bits_per_key, true, out_len);
+  return dlsm_batcher_submit(b, job, bits_per_key, DLSM_BATCH_HASHED, out_len);
 }
 
 int dlsm_batcher_stats(dlsm_batcher* b, uint64_t* batches, uint64_t* jobs, uint64_t* max_batch) {

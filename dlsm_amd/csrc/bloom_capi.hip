@@ -123,6 +123,11 @@ struct dlsm_ctx {
   uint64_t last_jobs_gen = 0, last_starts_gen = 0;
   DevBuf<LegacyJobDev> ljobs;
   DevBuf<uint64_t> lstarts;
+  // LDS-tiled legacy build (util/bloom.cc format)
+  DevBuf<LegacyTileJobDev> ltjobs;
+  DevBuf<uint32_t> ltstarts;  // chunk0s | slice0s
+  DevBuf<uint16_t> lentries;  // u16 bit positions per tile bucket
+  DevBuf<uint16_t> ltab;      // chunk-major tile-bucket offsets
   // probe workspace
   DevBuf<uint32_t> hashes;  // grouped probe: one BloomHash per lookup
   DevBuf<uint16_t> pos;
@@ -151,6 +156,17 @@ struct dlsm_ctx {
   void* host_buf = nullptr;
   uint64_t host_cap = 0;
   std::atomic<const void*> host_owner{nullptr};
+  // Page-locked sources of the small tables a call builds on the host and
+  // uploads asynchronously (job tables, rebased offsets, lengths, crc stream
+  // descriptors): a ring of slots, each reused only after the event recorded
+  // behind its copy has completed -- a pageable (e.g. stack) source could be
+  // gone before a queued copy reads it.
+  static constexpr int kUpSlots = 16;
+  uint8_t* up_buf[kUpSlots] = {};
+  uint64_t up_cap[kUpSlots] = {};
+  hipEvent_t up_ev[kUpSlots] = {};
+  bool up_live[kUpSlots] = {};
+  int up_next = 0;
 };
 
 // A stacked image of the filters of one mask byte that share a line count
@@ -317,6 +333,36 @@ int parse_tail(const uint8_t* tail, uint64_t len64, int* k_out, uint32_t* L_out,
   return DLSM_OK;
 }
 
+// Asynchronous H2D copy of n bytes of a host-built table (any memory, e.g.
+// a std::vector about to go out of scope) on stream s: the bytes are copied
+// into one of the context's page-locked upload slots first, so the caller's
+// buffer may be released as soon as this returns.  A slot is reused only
+// after the event behind its previous copy has completed.
+int ctx_upload(dlsm_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t s) {
+  if (n == 0) return DLSM_OK;
+  const int i = ctx->up_next;
+  ctx->up_next = (i + 1) % dlsm_ctx::kUpSlots;
+  if (ctx->up_live[i]) {
+    DLSM_TRY(hipEventSynchronize(ctx->up_ev[i]));
+    ctx->up_live[i] = false;
+  }
+  if (!ctx->up_ev[i]) DLSM_TRY(hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming));
+  if (ctx->up_cap[i] < n) {
+    if (ctx->up_buf[i]) (void)hipHostFree(ctx->up_buf[i]);
+    ctx->up_buf[i] = nullptr;
+    ctx->up_cap[i] = 0;
+    uint64_t c = 4096;
+    while (c < n) c <<= 1;
+    DLSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->up_buf[i]), c, hipHostMallocDefault));
+    ctx->up_cap[i] = c;
+  }
+  memcpy(ctx->up_buf[i], src, n);
+  DLSM_TRY(hipMemcpyAsync(dst, ctx->up_buf[i], n, hipMemcpyHostToDevice, s));
+  DLSM_TRY(hipEventRecord(ctx->up_ev[i], s));
+  ctx->up_live[i] = true;
+  return DLSM_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -376,6 +422,50 @@ int dlsm_device_count(int* n) {
   return e == hipSuccess ? DLSM_OK : from_hip(e);
 }
 
+}  // extern "C"
+namespace {
+// Per-thread contexts (dlsm_thread_ctx): owned = created here, destroyed at
+// the thread's exit; bound = the caller's (dlsm_thread_ctx_bind), never freed here.
+struct ThreadCtx {
+  dlsm_ctx* owned = nullptr;
+  dlsm_ctx* bound = nullptr;
+  ~ThreadCtx() {
+    if (owned) dlsm_ctx_destroy(owned);
+  }
+};
+ThreadCtx& thread_ctx_slot() {
+  thread_local ThreadCtx t;
+  return t;
+}
+std::atomic<unsigned> g_thread_ctx_next{0};
+}  // namespace
+extern "C" {
+
+int dlsm_thread_ctx(dlsm_ctx** out) {
+  if (!out) return DLSM_E_ARG;
+  ThreadCtx& t = thread_ctx_slot();
+  if (t.bound) {
+    *out = t.bound;
+    return DLSM_OK;
+  }
+  if (!t.owned) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n < 1) {
+      *out = nullptr;
+      return DLSM_E_DEVICE;
+    }
+    const int dev = static_cast<int>(g_thread_ctx_next.fetch_add(1) % static_cast<unsigned>(n));
+    DLSM_CHECK(dlsm_ctx_create(dev, &t.owned));
+  }
+  *out = t.owned;
+  return DLSM_OK;
+}
+
+int dlsm_thread_ctx_bind(dlsm_ctx* ctx) {
+  thread_ctx_slot().bound = ctx;
+  return DLSM_OK;
+}
+
 int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (!out) return DLSM_E_ARG;
   *out = nullptr;
@@ -421,6 +511,10 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->jobL.release();
   ctx->ljobs.release();
   ctx->lstarts.release();
+  ctx->ltjobs.release();
+  ctx->ltstarts.release();
+  ctx->lentries.release();
+  ctx->ltab.release();
   ctx->pos.release();
   ctx->hashes.release();
   ctx->smask.release();
@@ -447,6 +541,10 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   if (ctx->host_buf) (void)hipHostFree(ctx->host_buf);
   if (ctx->h_out) (void)hipHostFree(ctx->h_out);
   if (ctx->h_len) (void)hipHostFree(ctx->h_len);
+  for (int i = 0; i < dlsm_ctx::kUpSlots; i++) {
+    if (ctx->up_buf[i]) (void)hipHostFree(ctx->up_buf[i]);
+    if (ctx->up_ev[i]) (void)hipEventDestroy(ctx->up_ev[i]);
+  }
   delete ctx;
   return DLSM_OK;
 }
@@ -576,7 +674,8 @@ int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_byte
     b += buf.cap * sizeof(*buf.p);
   };
   add(ctx->entries); add(ctx->tab); add(ctx->jobs); add(ctx->starts); add(ctx->dchunk);
-  add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->pos); add(ctx->smask); add(ctx->hashes);
+  add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->ltjobs); add(ctx->ltstarts);
+  add(ctx->lentries); add(ctx->ltab); add(ctx->pos); add(ctx->smask); add(ctx->hashes);
   add(ctx->st_keys); add(ctx->st_offs); add(ctx->st_out); add(ctx->st_len); add(ctx->st_filter);
   add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_outp); add(ctx->crc_cap);
   add(ctx->crc_val); add(ctx->sel);
@@ -634,13 +733,21 @@ int dlsm_ctx_host_buffer(dlsm_ctx* ctx, uint64_t min_bytes, uint64_t keep_bytes,
 // Process-wide pool of page-locked host buffers (key staging of builders
 // that cannot borrow their context's buffer): a released buffer is kept and
 // handed to the next acquire that fits, so steady-state staging page-locks
-// nothing.  Sizes are powers of two >= 1 MiB.
+// nothing.  Sizes are powers of two >= 1 MiB.  At most kPoolKeepBytes of
+// released buffers are kept (a burst of builders does not pin host memory
+// for good); a release past that frees the buffer.
 }  // extern "C"
 namespace {
+constexpr uint64_t kPoolKeepBytes = uint64_t(1) << 30;
 struct HostPool {
   std::mutex m;
   std::multimap<uint64_t, void*> free_by_size;
-  std::unordered_map<void*, uint64_t> size_of;
+  struct Entry {
+    uint64_t size;
+    bool in_use;
+  };
+  std::unordered_map<void*, Entry> entry;
+  uint64_t free_bytes = 0;
 };
 HostPool& host_pool() {
   static HostPool p;
@@ -659,6 +766,8 @@ int dlsm_host_pool_acquire(uint64_t min_bytes, void** out, uint64_t* cap) {
     if (it != hp.free_by_size.end()) {
       *out = it->second;
       if (cap) *cap = it->first;
+      hp.free_bytes -= it->first;
+      hp.entry[it->second].in_use = true;
       hp.free_by_size.erase(it);
       return DLSM_OK;
     }
@@ -669,20 +778,33 @@ int dlsm_host_pool_acquire(uint64_t min_bytes, void** out, uint64_t* cap) {
   DLSM_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
   {
     std::lock_guard<std::mutex> lk(hp.m);
-    hp.size_of[p] = c;
+    hp.entry[p] = HostPool::Entry{c, true};
   }
   *out = p;
   if (cap) *cap = c;
   return DLSM_OK;
 }
 
+// DLSM_E_ARG for a pointer the pool did not hand out, or one already released
+// (a double release would give one buffer to two later acquirers).
 int dlsm_host_pool_release(void* p) {
   if (!p) return DLSM_OK;
   HostPool& hp = host_pool();
-  std::lock_guard<std::mutex> lk(hp.m);
-  auto it = hp.size_of.find(p);
-  if (it == hp.size_of.end()) return DLSM_E_ARG;
-  hp.free_by_size.emplace(it->second, p);
+  void* drop = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(hp.m);
+    auto it = hp.entry.find(p);
+    if (it == hp.entry.end() || !it->second.in_use) return DLSM_E_ARG;
+    if (hp.free_bytes + it->second.size > kPoolKeepBytes) {
+      drop = p;
+      hp.entry.erase(it);
+    } else {
+      it->second.in_use = false;
+      hp.free_by_size.emplace(it->second.size, p);
+      hp.free_bytes += it->second.size;
+    }
+  }
+  if (drop) DLSM_TRY(hipHostFree(drop));
   return DLSM_OK;
 }
 
@@ -691,9 +813,10 @@ int dlsm_host_pool_trim(void) {
   std::lock_guard<std::mutex> lk(hp.m);
   for (auto& kv : hp.free_by_size) {
     (void)hipHostFree(kv.second);
-    hp.size_of.erase(kv.second);
+    hp.entry.erase(kv.second);
   }
   hp.free_by_size.clear();
+  hp.free_bytes = 0;
   return DLSM_OK;
 }
 
@@ -797,10 +920,8 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
     ctx->last_jobs.clear();  // until the upload below is queued
     DLSM_CHECK(ctx->jobs.ensure(n_jobs));
     DLSM_CHECK(ctx->starts.ensure(2 * n_jobs));
-    DLSM_TRY(hipMemcpyAsync(ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs,
-                            hipMemcpyHostToDevice, s));
-    DLSM_TRY(hipMemcpyAsync(ctx->starts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs,
-                            hipMemcpyHostToDevice, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->jobs.p, hj.data(), sizeof(FullJobDev) * n_jobs, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->starts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs, s));
     ctx->last_jobs = hj;
     ctx->last_starts = starts;
     ctx->last_jobs_gen = ctx->jobs.gen;
@@ -892,10 +1013,7 @@ int stage_keys(dlsm_ctx* ctx, const dlsm_keyset* const* sets, int n, std::vector
       std::vector<uint64_t> ro(k.n + 1);
       for (uint64_t i = 0; i <= k.n; i++) ro[i] = k.offsets[i] - src0[j];
       d.offsets = ctx->st_offs.p + opos[j];
-      // pageable-source copies are staged before the call returns, so `ro`
-      // may be released right after.
-      DLSM_TRY(hipMemcpyAsync(const_cast<uint64_t*>(d.offsets), ro.data(),
-                              sizeof(uint64_t) * (k.n + 1), hipMemcpyHostToDevice, s));
+      DLSM_CHECK(ctx_upload(ctx, const_cast<uint64_t*>(d.offsets), ro.data(), sizeof(uint64_t) * (k.n + 1), s));
     }
     dev[j] = d;
   }
@@ -932,11 +1050,24 @@ uint8_t* host_device_view(void* p) {
   return static_cast<uint8_t*>(a.devicePointer) + off;
 }
 
-// Host keys -> host filters.  The keys go H2D into the context's staging; the
-// build kernels write each filter straight into the caller's slot when it is
-// page-locked (16-byte aligned), else into page-locked staging copied out
-// afterwards, and the lengths into page-locked memory: one stream
-// synchronisation per call and no device-to-host copy commands.
+// Whether full_build_dev_impl takes the sliced path for this batch (the
+// same choice it makes: not forced direct, and a slice width that fits).
+bool full_build_sliced(const dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key) {
+  if (ctx->path == 1) return false;
+  std::vector<uint32_t> Ls(n_jobs);
+  for (int j = 0; j < n_jobs; j++) Ls[j] = full_num_lines(jobs[j].keys.n, bits_per_key, nullptr);
+  return choose_build_lgR(Ls) >= 0;
+}
+
+// Host keys -> host filters.  The keys go H2D into the context's staging.
+// Sliced path: the slice kernels store each filter straight into the
+// caller's slot when it is page-locked (16-byte aligned), else into
+// page-locked staging copied out after the call, and the lengths into
+// page-locked memory -- one stream synchronisation per call and no
+// device-to-host copy commands; their stores are plain 16-byte writes.  The
+// direct path (forced, or a batch too large to slice) sets bits with global
+// atomics, which must not target host memory (that would need PCIe
+// AtomicOps): it builds into device staging and copies the filters out.
 int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
                          uint64_t* out_len, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
@@ -948,6 +1079,7 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
     if (!jobs[j].out) return DLSM_E_ARG;
     sets[j] = &jobs[j].keys;
   }
+  const bool to_host = full_build_sliced(ctx, jobs, n_jobs, bits_per_key);
   std::vector<dlsm_keyset> dk;
   DLSM_CHECK(stage_keys(ctx, sets.data(), n_jobs, dk));
   std::vector<dlsm_build_job> dj(n_jobs);
@@ -957,12 +1089,31 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
   for (int j = 0; j < n_jobs; j++) {
     const uint64_t spec = full_filter_len(jobs[j].keys.n, bits_per_key);
     const uint64_t cap = std::min(spec, jobs[j].out_cap);
-    direct[j] = host_device_view(jobs[j].out);
+    direct[j] = to_host ? host_device_view(jobs[j].out) : nullptr;
     if (direct[j] && !aligned(direct[j], 16)) direct[j] = nullptr;
     opos[j] = obytes;
     if (!direct[j]) obytes += (cap + 255) & ~uint64_t(255);
     dj[j].keys = dk[j];
     dj[j].out_cap = cap;
+  }
+  hipStream_t s = ctx->stream;
+  if (!to_host) {
+    DLSM_CHECK(ctx->st_out.ensure(obytes + 256));
+    DLSM_CHECK(ctx->st_len.ensure(n_jobs));
+    for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
+    DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p, hashed));
+    DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
+    DLSM_TRY(hipStreamSynchronize(s));
+    int st = DLSM_OK;
+    for (int j = 0; j < n_jobs; j++) {
+      if (out_len[j] == 0) {
+        st = DLSM_E_CAPACITY;
+        continue;
+      }
+      DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
+    }
+    DLSM_TRY(hipStreamSynchronize(s));
+    return st;
   }
   DLSM_CHECK(host_ensure(ctx->h_out, ctx->h_out_cap, obytes + 256));
   DLSM_CHECK(host_ensure(ctx->h_len, ctx->h_len_cap, static_cast<uint64_t>(n_jobs)));
@@ -971,7 +1122,7 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
   if (!h_out_dev || !h_len_dev) return DLSM_E_DEVICE;
   for (int j = 0; j < n_jobs; j++) dj[j].out = direct[j] ? direct[j] : h_out_dev + opos[j];
   DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, h_len_dev, hashed));
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  DLSM_TRY(hipStreamSynchronize(s));
   int st = DLSM_OK;
   for (int j = 0; j < n_jobs; j++) {
     out_len[j] = ctx->h_len[j];
@@ -1034,14 +1185,14 @@ int run_crc(dlsm_ctx* ctx, const std::vector<std::vector<uint8_t>>& streams, int
   DLSM_CHECK(ctx->crc_partial.ensure(static_cast<size_t>(max_parts) * n));
   std::vector<uint8_t> flat(ss * n);
   for (int j = 0; j < n; j++) memcpy(flat.data() + ss * j, streams[j].data(), ss);
-  DLSM_TRY(hipMemcpyAsync(ctx->crc_streams.p, flat.data(), ss * n, hipMemcpyHostToDevice, s));
+  DLSM_CHECK(ctx_upload(ctx, ctx->crc_streams.p, flat.data(), ss * n, s));
   uint8_t* const* seal_out = nullptr;
   const uint64_t* seal_cap = nullptr;
   if (seal_out_host) {
     DLSM_CHECK(ctx->crc_outp.ensure(n));
     DLSM_CHECK(ctx->crc_cap.ensure(n));
-    DLSM_TRY(hipMemcpyAsync(ctx->crc_outp.p, seal_out_host, sizeof(uint8_t*) * n, hipMemcpyHostToDevice, s));
-    DLSM_TRY(hipMemcpyAsync(ctx->crc_cap.p, seal_cap_host, sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->crc_outp.p, seal_out_host, sizeof(uint8_t*) * n, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->crc_cap.p, seal_cap_host, sizeof(uint64_t) * n, s));
     seal_out = ctx->crc_outp.p;
     seal_cap = ctx->crc_cap.p;
   }
@@ -1856,6 +2007,24 @@ int dlsm_version_probe_dev(dlsm_ctx* ctx, const dlsm_version* v, const dlsm_keys
 // ---------------------------------------------------------------------------
 // Legacy FilterPolicy format (util/bloom.cc)
 // ---------------------------------------------------------------------------
+namespace {
+// Tiles per legacy slice workgroup (log2): 16 (128 KiB of LDS, one workgroup
+// per CU) unless the batch then has fewer slices than the chip has CUs.
+int choose_legacy_tps_lg(const std::vector<uint32_t>& n_tiles) {
+  if (const char* e = getenv("DLSM_LEGACY_TPS_LG")) {
+    const int v = atoi(e);
+    if (v >= 0 && v <= 4) return v;
+  }
+  int lg = 4;
+  for (; lg > 0; lg--) {
+    uint64_t total = 0;
+    for (uint32_t t : n_tiles) total += (t + (1u << lg) - 1) >> lg;
+    if (total >= kBuildSliceCUs) break;
+  }
+  return lg;
+}
+}  // namespace
+
 int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
                                 int bits_per_key, uint64_t* out_len_dev) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
@@ -1863,9 +2032,11 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   const int k = legacy_num_probes(bits_per_key);
-  bool all_k20 = true;
+  bool all_k20 = true, all_k28 = true;
+  bool fits_a = k <= kLegacyKmaxA, fits_b = k <= kLegacyKmaxB;
   uint64_t ws = 0, total = 0;
   std::vector<uint64_t> wpos(n_jobs), lens(n_jobs);
+  std::vector<uint32_t> tiles(n_jobs), regions(n_jobs);
   for (int j = 0; j < n_jobs; j++) {
     DLSM_CHECK(validate_keyset(jobs[j].keys));
     if (!jobs[j].out) return DLSM_E_ARG;
@@ -1875,9 +2046,63 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
     wpos[j] = ws;
     ws += (bits / 8 + 3 + 255) & ~uint64_t(255);
     all_k20 = all_k20 && is_k20(jobs[j].keys);
+    all_k28 = all_k28 && is_k28(jobs[j].keys);
+    // the LDS-tiled path: positions as u16 inside 2^16-bit tiles, one chunk's
+    // region (k positions per key + up to 7 pads per tile) staged in LDS
+    const uint64_t nt = (bits + (uint64_t(1) << kLegacyTileLg) - 1) >> kLegacyTileLg;
+    const uint64_t reg = (static_cast<uint64_t>(k) * kLegacyChunk + 7 * nt + 7) & ~uint64_t(7);
+    tiles[j] = static_cast<uint32_t>(std::min<uint64_t>(nt, 0xffffffffu));
+    regions[j] = static_cast<uint32_t>(std::min<uint64_t>(reg, 0xffffffffu));
+    const bool ok = bits <= 0xffffffffull && jobs[j].keys.n <= 0x7fffffffull * kLegacyChunk;
+    fits_a = fits_a && ok && nt <= kLegacyTilesA && reg <= kLegacyStageA;
+    fits_b = fits_b && ok && nt <= kLegacyTilesB && reg <= kLegacyStageB;
   }
-  const int mode = all_k20 ? KM_K20 : KM_GENERIC;
-  // Build into an aligned workspace (word atomics), then copy to the slots.
+  const int mode = all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC);
+  if (ctx->path != 1 && fits_b) {
+    const int tps_lg = choose_legacy_tps_lg(tiles);
+    std::vector<LegacyTileJobDev> hj(n_jobs);
+    std::vector<uint32_t> starts(2 * n_jobs);
+    uint64_t entry = 0, tabw = 0;
+    uint32_t chunk = 0, slice = 0;
+    for (int j = 0; j < n_jobs; j++) {
+      LegacyTileJobDev& d = hj[j];
+      const uint64_t bits = legacy_bits(jobs[j].keys.n, bits_per_key);
+      d.keys = to_desc(jobs[j].keys);
+      d.out = jobs[j].out;
+      d.out_len = out_len_dev + j;
+      d.entry0 = entry;
+      d.tab0 = tabw;
+      d.bits = static_cast<uint32_t>(bits);
+      d.magic = fastmod_magic(d.bits);
+      d.n_tiles = tiles[j];
+      d.region = regions[j];
+      d.n_chunks = ceil_div_u32(jobs[j].keys.n, kLegacyChunk);
+      d.chunk0 = chunk;
+      d.n_slices = (tiles[j] + (1u << tps_lg) - 1) >> tps_lg;
+      d.slice0 = slice;
+      d.k = k;
+      d.reserved = 0;
+      starts[j] = chunk;
+      starts[n_jobs + j] = slice;
+      entry += static_cast<uint64_t>(d.n_chunks) * d.region;
+      tabw += static_cast<uint64_t>(d.n_chunks) * (d.n_tiles + 1);
+      chunk += d.n_chunks;
+      slice += d.n_slices;
+    }
+    DLSM_CHECK(ctx->ltjobs.ensure(n_jobs));
+    DLSM_CHECK(ctx->ltstarts.ensure(2 * n_jobs));
+    DLSM_CHECK(ctx->lentries.ensure(entry + 8));
+    DLSM_CHECK(ctx->ltab.ensure(tabw + 1));
+    DLSM_CHECK(ctx_upload(ctx, ctx->ltjobs.p, hj.data(), sizeof(LegacyTileJobDev) * n_jobs, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->ltstarts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs, s));
+    DLSM_TRY(launch_legacy_partition(ctx->ltjobs.p, ctx->ltstarts.p, n_jobs, chunk, ctx->lentries.p, ctx->ltab.p,
+                                     fits_a ? 0 : 1, mode, s));
+    DLSM_TRY(launch_legacy_slices(ctx->ltjobs.p, ctx->ltstarts.p + n_jobs, n_jobs, slice, ctx->lentries.p,
+                                  ctx->ltab.p, tps_lg, s));
+    return DLSM_OK;
+  }
+  if (ctx->path == 2) return DLSM_E_ARG;  // sliced forced, but the batch does not fit it
+  // Direct path: global atomics into an aligned workspace, then copies to the slots.
   DLSM_CHECK(ctx->st_filter.ensure(ws + 256));
   DLSM_TRY(hipMemsetAsync(ctx->st_filter.p, 0, ws, s));
   for (int j0 = 0; j0 < n_jobs; j0 += 256) {
@@ -1900,9 +2125,9 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
     total += tk;
     DLSM_CHECK(ctx->ljobs.ensure(nj));
     DLSM_CHECK(ctx->lstarts.ensure(nj));
-    DLSM_TRY(hipMemcpyAsync(ctx->ljobs.p, hj.data(), sizeof(LegacyJobDev) * nj, hipMemcpyHostToDevice, s));
-    DLSM_TRY(hipMemcpyAsync(ctx->lstarts.p, key0s.data(), sizeof(uint64_t) * nj, hipMemcpyHostToDevice, s));
-    DLSM_TRY(launch_legacy_scatter(ctx->ljobs.p, ctx->lstarts.p, nj, tk, mode, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->ljobs.p, hj.data(), sizeof(LegacyJobDev) * nj, s));
+    DLSM_CHECK(ctx_upload(ctx, ctx->lstarts.p, key0s.data(), sizeof(uint64_t) * nj, s));
+    DLSM_TRY(launch_legacy_scatter(ctx->ljobs.p, ctx->lstarts.p, nj, tk, mode == KM_K20 ? KM_K20 : KM_GENERIC, s));
     // the job table is reused by the next group: keep the stream ordered
   }
   for (int j = 0; j < n_jobs; j++) {
@@ -1910,7 +2135,7 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
                             hipMemcpyDeviceToDevice, s));
     DLSM_TRY(hipMemsetAsync(jobs[j].out + lens[j] - 1, static_cast<int>(static_cast<uint8_t>(k)), 1, s));
   }
-  DLSM_TRY(hipMemcpyAsync(out_len_dev, lens.data(), sizeof(uint64_t) * n_jobs, hipMemcpyHostToDevice, s));
+  DLSM_CHECK(ctx_upload(ctx, out_len_dev, lens.data(), sizeof(uint64_t) * n_jobs, s));
   (void)total;
   return DLSM_OK;
 }

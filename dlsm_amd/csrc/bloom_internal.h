@@ -87,6 +87,53 @@ struct LegacyJobDev {
   uint64_t key0;      // global index of this job's first key (flattened grid)
 };
 
+// Legacy-format build job of the LDS-tiled path (util/bloom.cc:25-55).  The
+// filter's bits are cut into tiles of 2^16 bits (8 KiB); the partition pass
+// writes every bit position a key sets as a u16 offset inside its tile,
+// bucketed by tile inside the key's kLegacyChunk-key chunk (each bucket padded
+// to 8 entries = one 16-byte unit with copies of one of its positions: OR-ing
+// a bit twice changes nothing), and the slice pass ORs 2^tps_lg tiles in LDS.
+struct LegacyTileJobDev {
+  KeyDesc keys;
+  uint8_t* out;
+  uint64_t* out_len;   // device slot for this job's length (bytes + 1)
+  uint64_t entry0;     // first u16 of this job's chunk regions
+  uint64_t tab0;       // first u16 of this job's n_chunks x (n_tiles+1) bucket-offset table
+  uint32_t bits;       // filter bits (multiple of 8, < 2^32)
+  uint32_t magic;      // fastmod magic for bits
+  uint32_t n_tiles;    // ceil(bits / 2^16)
+  uint32_t region;     // u16 entries per chunk region (multiple of 8)
+  uint32_t chunk0, n_chunks;
+  uint32_t slice0, n_slices;
+  int32_t k;
+  int32_t reserved;
+};
+constexpr uint32_t kLegacyTileLg = 16;  // bits per tile: 2^16 (8 KiB of LDS)
+#ifndef DLSM_LEGACY_CHUNK
+#define DLSM_LEGACY_CHUNK 2048  // keys per legacy partition chunk
+#endif
+#ifndef DLSM_LEGACY_NT
+#define DLSM_LEGACY_NT 256      // threads per legacy partition workgroup
+#endif
+#ifndef DLSM_LEGACY_RANKED
+#define DLSM_LEGACY_RANKED 0    // 1: one ranked atomic pass (ranks kept in registers)
+#endif
+constexpr int kLegacyChunk = DLSM_LEGACY_CHUNK;
+constexpr int kLegacyPartBlock = DLSM_LEGACY_NT;
+// Partition variants (static LDS staging of one chunk region of u16 entries:
+// k positions per key + up to 7 pads per tile): A: k <= 6, <= 512 tiles;
+// B: k <= 8, <= 4 x threads - 1 tiles (the bins one block scan covers: 1,023
+// tiles = 64 Mbit at 256 threads).  Larger filters or k take the direct
+// (global atomic) path.
+constexpr int kLegacyKmaxA = 6, kLegacyKmaxB = 8;
+constexpr uint32_t kLegacyTilesA = 512, kLegacyTilesB = 4u * kLegacyPartBlock - 1u;
+constexpr uint32_t legacy_region(int k, uint32_t tiles) {
+  return (static_cast<uint32_t>(k) * kLegacyChunk + 7u * tiles + 7u) & ~7u;
+}
+constexpr uint32_t kLegacyStageA = legacy_region(kLegacyKmaxA, kLegacyTilesA);
+constexpr uint32_t kLegacyStageB = legacy_region(kLegacyKmaxB, kLegacyTilesB);
+constexpr int kLegacySliceBlock = 1024;
+
 constexpr int kBlock = 256;
 constexpr int kMaxSlices = 256;     // slice bins per table in one partition pass
 constexpr uint32_t kBuildSliceCUs = 256;  // MI355X CUs: the build's slice-count target (choose_build_lgR)
@@ -177,6 +224,14 @@ hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,
                                int trivial, KeyDesc keys, uint8_t* out, int mode, hipStream_t s);
+// LDS-tiled legacy build: variant 0 = A, 1 = B (kLegacy*); tps_lg 0..4 tiles
+// per slice workgroup (log2).
+hipError_t launch_legacy_partition(const LegacyTileJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                                   uint32_t total_chunks, uint16_t* entries, uint16_t* tab, int variant,
+                                   int mode, hipStream_t s);
+hipError_t launch_legacy_slices(const LegacyTileJobDev* jobs, const uint32_t* slice0s, int n_jobs,
+                                uint32_t total_slices, const uint16_t* entries, const uint16_t* tab, int tps_lg,
+                                hipStream_t s);
 
 // key_select.hip: internal-key selection (flush / compaction drop rules) and
 // the packing of kept user keys.  Workspace: blk_cnt / blk_bytes hold

@@ -1729,6 +1729,292 @@ __global__ __launch_bounds__(kBlock) void legacy_probe_kernel(const uint8_t* __r
   }
 }
 
+// ---------------------------------------------------------------------------
+// Legacy FilterPolicy build, LDS-tiled (util/bloom.cc:25-55).  The legacy
+// format spreads a key's k bits over the WHOLE filter (bitpos = h % bits,
+// then h += rotr(h, 17)), so the unit the build buckets is one bit position,
+// not one key.  Pass 1 (partition, one 512-thread workgroup per 4,096-key
+// chunk): hash each key once, compute its k positions, and bucket them by
+// 8 KiB tile (2^16 bits) as u16 offsets inside the tile -- 2k bytes per key;
+// every bucket is padded to whole 16-byte units with copies of its first
+// entry (setting a bit twice changes nothing).  Pass 2 (slice, one
+// 1,024-thread workgroup per 2^TPS_LG consecutive tiles of one filter): the
+// tiles live in LDS, every wave walks its share of the chunks (one contiguous
+// run per chunk: the slice's buckets are adjacent), sets bits with ds_or and
+// the tiles stream out with 16-byte stores.  No global atomics: the direct
+// kernel's 6 device-scope atomicOr per key are memory-side operations on
+// 64 random rows per wave instruction.
+// ---------------------------------------------------------------------------
+template <int MODE, int KMAX, uint32_t STAGE, uint32_t TMAX>
+__global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
+    const LegacyTileJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
+    uint16_t* __restrict__ entries, uint16_t* __restrict__ tab) {
+  constexpr int NT = kLegacyPartBlock;
+  constexpr int C = kLegacyChunk;
+  constexpr int PER = C / NT;
+  constexpr int KB = mode_kb<MODE>();
+  constexpr int TKV = K20Tile<NT, tile_kpt<KB>(), KB>::kVec;  // uint4 of one key tile
+  constexpr int SV = static_cast<int>(STAGE / 8u);            // uint4 of one staged region
+  constexpr int TVB = TKV > SV ? TKV : SV;
+  static_assert(TMAX + 1 <= 4u * NT, "block_excl_scan_lds covers the tile bins");
+  __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
+  __shared__ uint32_t hist[TMAX + 1];
+  __shared__ uint8_t npad[TMAX];
+  __shared__ uint32_t wsum[NT / 64];
+  __shared__ int sj;
+  const int tid = threadIdx.x;
+  const uint32_t bid = blockIdx.x;
+  if (tid == 0) sj = find_job(chunk0s, n_jobs, bid);
+  __syncthreads();
+  const LegacyTileJobDev J = jobs[sj];
+  const uint32_t c = bid - J.chunk0;
+  const uint64_t first = static_cast<uint64_t>(c) * C;
+  const uint64_t left = J.keys.n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+  uint32_t h[PER];
+  hash_chunk<MODE, NT, PER>(J.keys, first, nk, tile, h);
+  const uint32_t nT = J.n_tiles, bits = J.bits, magic = J.magic;
+  const int k = J.k;
+  for (uint32_t b = tid; b <= nT; b += NT) hist[b] = 0;
+  __syncthreads();
+#if DLSM_LEGACY_RANKED
+  // one ranked pass: each position's rank inside its tile bucket (u16, two
+  // per register); the scatter recomputes the position and reads its
+  // bucket's start
+  uint32_t rk[(PER * KMAX + 1) / 2];
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
+    uint32_t hh = h[r];
+    const uint32_t delta = bloom_delta(hh);
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      const int x = r * KMAX + q;
+      if (live && q < k) {
+        const uint32_t rank = atomicAdd(&hist[fastmod(hh, bits, magic) >> kLegacyTileLg], 1u);
+        rk[x >> 1] = (x & 1) ? (rk[x >> 1] | (rank << 16)) : rank;
+      }
+      hh += delta;
+    }
+  }
+#else
+  // Count the positions per tile (the positions are computed twice -- here
+  // and in the scatter -- rather than kept: 8 keys x k codes per thread would
+  // hold ~50 more VGPRs and halve the workgroups per CU).
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
+    uint32_t hh = h[r];
+    const uint32_t delta = bloom_delta(hh);
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      if (live && q < k) atomicAdd(&hist[fastmod(hh, bits, magic) >> kLegacyTileLg], 1u);
+      hh += delta;
+    }
+  }
+#endif
+  __syncthreads();
+  for (uint32_t b = tid; b < nT; b += NT) {  // pad every bucket to whole 16-byte units
+    const uint32_t cnt = hist[b];
+    const uint32_t pad = (0u - cnt) & 7u;
+    npad[b] = static_cast<uint8_t>(pad);
+    hist[b] = cnt + pad;
+  }
+  __syncthreads();
+  const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(nT + 1), wsum);
+  uint16_t* trow = tab + J.tab0 + static_cast<uint64_t>(c) * (nT + 1);
+  for (uint32_t b = tid; b <= nT; b += NT) trow[b] = static_cast<uint16_t>(hist[b]);
+  uint16_t* stage = reinterpret_cast<uint16_t*>(tile);  // free since hash_chunk's last barrier
+#if DLSM_LEGACY_RANKED
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
+    uint32_t hh = h[r];
+    const uint32_t delta = bloom_delta(hh);
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      const int x = r * KMAX + q;
+      if (live && q < k) {
+        const uint32_t bp = fastmod(hh, bits, magic);
+        const uint32_t rank = (x & 1) ? (rk[x >> 1] >> 16) : (rk[x >> 1] & 0xffffu);
+        stage[hist[bp >> kLegacyTileLg] + rank] = static_cast<uint16_t>(bp);
+      }
+      hh += delta;
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = tid; b < nT; b += NT) {  // pads: copies of the bucket's last position
+    const uint32_t np = npad[b];
+    if (np) {
+      const uint32_t end = hist[b + 1] - np;
+      const uint16_t v = stage[end - 1];
+      for (uint32_t p = 0; p < np; p++) stage[end + p] = v;
+    }
+  }
+#else
+  __syncthreads();  // hist becomes the buckets' fill cursors
+  // Scatter: a bucket's order is whatever the LDS atomics give -- the slice
+  // pass ORs bits, so the order of a tile's positions never shows.
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
+    uint32_t hh = h[r];
+    const uint32_t delta = bloom_delta(hh);
+#pragma unroll
+    for (int q = 0; q < KMAX; q++) {
+      if (live && q < k) {
+        const uint32_t bp = fastmod(hh, bits, magic);
+        stage[atomicAdd(&hist[bp >> kLegacyTileLg], 1u)] = static_cast<uint16_t>(bp);
+      }
+      hh += delta;
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = tid; b < nT; b += NT) {  // pads: copies of the bucket's last position
+    const uint32_t np = npad[b];
+    if (np) {
+      const uint32_t end = hist[b];  // the cursor stopped after the last real position
+      const uint16_t v = stage[end - 1];
+      for (uint32_t p = 0; p < np; p++) stage[end + p] = v;
+    }
+  }
+#endif
+  __syncthreads();
+  store_chunk_u16<NT>(entries + J.entry0 + static_cast<uint64_t>(c) * J.region, stage, total);
+}
+
+// One chunk's run of a legacy slice, as one wave sees it: lane j <= tn holds
+// the table row's offset of tile t0 + j (u16 entries); r0 / T / the unit
+// offsets of the tile starts are wave-uniform.
+struct LegacyRun {
+  uint32_t r0, T;           // first entry of the run, its length in 16-byte units
+  uint32_t ts[15];          // unit offset of tile j + 1 inside the run (j < tn - 1)
+  const uint4* base;
+};
+
+template <uint32_t TPS>
+__device__ __forceinline__ LegacyRun legacy_run(uint32_t row, uint32_t tn, const uint16_t* ent,
+                                                uint64_t region_off) {
+  LegacyRun R;
+  R.r0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), 0));
+  const uint32_t rend = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), static_cast<int>(tn)));
+  R.T = (rend - R.r0) >> 3;
+#pragma unroll
+  for (uint32_t j = 0; j + 1 < TPS; j++) {
+    const uint32_t lj = min(j + 1u, tn);
+    R.ts[j] = (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(row), static_cast<int>(lj))) - R.r0) >> 3;
+  }
+  R.base = reinterpret_cast<const uint4*>(ent + region_off + R.r0);
+  return R;
+}
+
+// OR the 8 positions of unit u (of run R) into the slice's LDS tiles.
+template <uint32_t TPS>
+__device__ __forceinline__ void legacy_or_unit(uint32_t* sl, const LegacyRun& R, uint32_t u, const uint4& v) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t j = 0; j + 1 < TPS; j++) m += u >= R.ts[j] ? 1u : 0u;  // tiles past tn repeat the run's end
+  uint32_t* t = sl + (m << 11);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint32_t lo = w[q] & 0xffffu, hi = w[q] >> 16;
+    atomicOr(&t[lo >> 5], 1u << (lo & 31u));
+    atomicOr(&t[hi >> 5], 1u << (hi & 31u));
+  }
+}
+
+template <int TPS_LG>
+__global__ __launch_bounds__(kLegacySliceBlock) void legacy_slice_kernel(
+    const LegacyTileJobDev* __restrict__ jobs, const uint32_t* __restrict__ slice0s, int n_jobs,
+    const uint16_t* __restrict__ entries, const uint16_t* __restrict__ tab) {
+  constexpr uint32_t TPS = 1u << TPS_LG;
+  constexpr int NW = kLegacySliceBlock / 64;
+  constexpr int UPL = 4;  // units in flight per lane per chunk (256 units = 2,048 positions)
+  __shared__ __attribute__((aligned(16))) uint32_t sl[TPS * 2048u];
+  __shared__ int sj;
+  const int tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wv = static_cast<uint32_t>(wave_id());
+  const uint32_t bid = xcd_block(blockIdx.x, gridDim.x);
+  if (tid == 0) sj = find_job(slice0s, n_jobs, bid);
+  for (uint32_t w = tid; w < TPS * 512u; w += kLegacySliceBlock) reinterpret_cast<uint4*>(sl)[w] = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  const LegacyTileJobDev J = jobs[sj];
+  const uint32_t s = bid - J.slice0;
+  const uint32_t t0 = s << TPS_LG;
+  const uint32_t nT = J.n_tiles;
+  const uint32_t tn = min(TPS, nT - t0);
+  const uint32_t nC = J.n_chunks, rowlen = nT + 1;
+  const uint16_t* tb = tab + J.tab0 + t0;
+  const uint16_t* ent = entries + J.entry0;
+  // Row loads are clamped (unconditional); a wave works chunk c while chunk
+  // c + NW's row and units are already in flight.
+  auto row_at = [&](uint32_t cc) -> uint32_t {
+    const uint32_t c1 = min(cc, nC - 1u);
+    return tb[static_cast<uint64_t>(c1) * rowlen + min(lane, tn)];
+  };
+  auto fetch = [&](const LegacyRun& R, uint4 (&v)[UPL]) {
+#pragma unroll
+    for (int i = 0; i < UPL; i++) {
+      const uint32_t u = min(lane + 64u * i, R.T - 1u);  // T > 0 when fetched
+      v[i] = R.base[u];
+    }
+  };
+  auto consume = [&](const LegacyRun& R, const uint4 (&v)[UPL]) {
+#pragma unroll
+    for (int i = 0; i < UPL; i++) {
+      const uint32_t u = lane + 64u * i;
+      if (u < R.T) legacy_or_unit<TPS>(sl, R, u, v[i]);
+    }
+    for (uint32_t u = lane + 64u * UPL; u < R.T; u += 64u) legacy_or_unit<TPS>(sl, R, u, R.base[u]);  // long runs
+  };
+  uint32_t c = wv;
+  if (c < nC) {
+    uint32_t rowA = row_at(c);
+    uint32_t rowN = row_at(c + NW);
+    LegacyRun A = legacy_run<TPS>(rowA, tn, ent, static_cast<uint64_t>(c) * J.region);
+    uint4 vA[UPL];
+    if (A.T) fetch(A, vA);
+    while (true) {
+      const uint32_t cn = c + NW;
+      const bool more = cn < nC;
+      LegacyRun B;
+      uint4 vB[UPL];
+      if (more) {
+        B = legacy_run<TPS>(rowN, tn, ent, static_cast<uint64_t>(cn) * J.region);
+        if (B.T) fetch(B, vB);
+        rowN = row_at(cn + NW);
+      }
+      if (A.T) consume(A, vA);
+      if (!more) break;
+      A = B;
+#pragma unroll
+      for (int i = 0; i < UPL; i++) vA[i] = vB[i];
+      c = cn;
+    }
+  }
+  __syncthreads();
+  // Stream the tiles out: bytes [t0 * 8 KiB, min((t0 + tn) * 8 KiB, bits / 8)).
+  const uint64_t bytes = J.bits / 8u;
+  const uint64_t b0 = static_cast<uint64_t>(t0) << (kLegacyTileLg - 3);
+  const uint64_t nb = min(static_cast<uint64_t>(tn) << (kLegacyTileLg - 3), bytes - b0);
+  uint8_t* dst = J.out + b0;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(sl);
+  if ((reinterpret_cast<uintptr_t>(J.out) & 15u) == 0) {
+    const uint32_t nv = static_cast<uint32_t>(nb >> 4);
+    for (uint32_t w = tid; w < nv; w += kLegacySliceBlock)
+      reinterpret_cast<uint4*>(dst)[w] = reinterpret_cast<const uint4*>(src)[w];
+    for (uint32_t i = nv * 16u + tid; i < nb; i += kLegacySliceBlock) dst[i] = src[i];
+  } else {
+    for (uint32_t i = tid; i < nb; i += kLegacySliceBlock) dst[i] = src[i];
+  }
+  if (s == 0 && tid == 0) {
+    J.out[bytes] = static_cast<uint8_t>(static_cast<int8_t>(J.k));  // dst->append(&hash_num, 1)
+    *J.out_len = bytes + 1u;
+  }
+}
+
 inline unsigned grid_for(uint64_t n, unsigned cap = 256u * 16u) {
   const uint64_t g = (n + kBlock - 1) / kBlock;
   return static_cast<unsigned>(g < 1 ? 1 : (g > cap ? cap : g));
@@ -2279,6 +2565,44 @@ hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t ma
     legacy_probe_kernel<KM_K20><<<g, kBlock, 0, s>>>(filter, bits, magic, k, trivial, keys, out);
   else
     legacy_probe_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(filter, bits, magic, k, trivial, keys, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_legacy_partition(const LegacyTileJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
+                                   uint32_t total_chunks, uint16_t* entries, uint16_t* tab, int variant,
+                                   int mode, hipStream_t s) {
+  if (total_chunks == 0) return hipSuccess;
+#define DLSM_LPART(MM, KM, ST, TM) \
+  legacy_partition_kernel<MM, KM, ST, TM><<<total_chunks, kLegacyPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, entries, tab)
+#define DLSM_LPART_V(MM)                                                   \
+  do {                                                                     \
+    if (variant == 0) DLSM_LPART(MM, kLegacyKmaxA, kLegacyStageA, kLegacyTilesA); \
+    else DLSM_LPART(MM, kLegacyKmaxB, kLegacyStageB, kLegacyTilesB);          \
+  } while (0)
+  if (mode == KM_K20) DLSM_LPART_V(KM_K20);
+  else if (mode == KM_K28) DLSM_LPART_V(KM_K28);
+  else DLSM_LPART_V(KM_GENERIC);
+#undef DLSM_LPART_V
+#undef DLSM_LPART
+  return hipGetLastError();
+}
+
+hipError_t launch_legacy_slices(const LegacyTileJobDev* jobs, const uint32_t* slice0s, int n_jobs,
+                                uint32_t total_slices, const uint16_t* entries, const uint16_t* tab, int tps_lg,
+                                hipStream_t s) {
+  if (total_slices == 0) return hipSuccess;
+  switch (tps_lg) {
+#define DLSM_LSL(T) \
+  case T: legacy_slice_kernel<T><<<total_slices, kLegacySliceBlock, 0, s>>>(jobs, slice0s, n_jobs, entries, tab); break
+    DLSM_LSL(0);
+    DLSM_LSL(1);
+    DLSM_LSL(2);
+    DLSM_LSL(3);
+    DLSM_LSL(4);
+#undef DLSM_LSL
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

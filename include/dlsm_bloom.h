@@ -117,6 +117,16 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx);
  * restores the context's own stream. */
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
 void* dlsm_ctx_stream(dlsm_ctx* ctx);
+/* The calling thread's context: the one bound with dlsm_thread_ctx_bind, else
+ * one the library creates on the thread's first call -- on device (i mod
+ * device count) for the i-th thread that asks -- and destroys when the thread
+ * exits.  dLSM runs each TableBuilder on one thread (flush / compaction /
+ * subcompaction threads, include/TimberSaw/options.h:73-78), so a
+ * FullFilterBlockBuilder with the reference's (ibv_mr*, bits_per_key)
+ * signature (table/full_filter_block.h:35) takes its context from here. */
+int dlsm_thread_ctx(dlsm_ctx** out);
+/* Bind a context the caller owns (NULL: unbind) as the calling thread's. */
+int dlsm_thread_ctx_bind(dlsm_ctx* ctx);
 /* The device a context runs on (-1 for NULL). */
 int dlsm_ctx_device(const dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
@@ -185,8 +195,10 @@ int dlsm_host_alloc(size_t len, void** out);
 int dlsm_host_free(void* p);
 /* A process-wide pool of page-locked host buffers: acquire returns a buffer
  * of at least min_bytes (*cap: its size), reusing a released one when one
- * fits; release returns it to the pool (only pool buffers); trim frees every
- * buffer in the pool.  For key staging of builders that share no context. */
+ * fits; release returns it to the pool (DLSM_E_ARG for a pointer the pool
+ * did not hand out or one already released); trim frees every buffer in the
+ * pool.  At most 1 GiB of released buffers is kept: a release past that frees
+ * the buffer.  For key staging of builders that share no context. */
 int dlsm_host_pool_acquire(uint64_t min_bytes, void** out, uint64_t* cap);
 int dlsm_host_pool_release(void* p);
 int dlsm_host_pool_trim(void);
@@ -247,6 +259,17 @@ int dlsm_batcher_destroy(dlsm_batcher* b);
 int dlsm_batcher_full_build(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, uint64_t* out_len);
 int dlsm_batcher_full_build_hashed(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key,
                                    uint64_t* out_len);
+/* The general form: flags DLSM_BATCH_HASHED (the keys are BloomHash values,
+ * as dlsm_batcher_full_build_hashed) | DLSM_BATCH_EXACT (the builder saw
+ * repeated keys: the executor counts the line number exactly before
+ * bucketing, DLSM_OPT_BUILD_EXACT = 1).  Jobs are batched only with jobs of
+ * the same bits_per_key and flags.  A job whose batch fails for another
+ * reason than a small slot is re-run alone, so each caller gets its own
+ * status. */
+#define DLSM_BATCH_HASHED 1
+#define DLSM_BATCH_EXACT 2
+int dlsm_batcher_submit(dlsm_batcher* b, const dlsm_build_job* job, int bits_per_key, int flags,
+                        uint64_t* out_len);
 /* Batches run, jobs built, and the largest batch so far. */
 int dlsm_batcher_stats(dlsm_batcher* b, uint64_t* batches, uint64_t* jobs, uint64_t* max_batch);
 

@@ -32,6 +32,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #if defined(__x86_64__)
 #include <immintrin.h>
@@ -224,9 +225,42 @@ inline size_t DedupStore16(const uint32_t*, size_t, uint32_t, bool, uint8_t*) { 
 #endif
 
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
+// (The reference-signature constructor below takes any type with `addr` and
+// `length` -- ibv_mr itself binds as-is.)
 struct FilterSlot {
   void* addr;
   size_t length;
+};
+
+// The calling thread's context (dlsm_thread_ctx): created by the library on
+// the thread's first builder, on the i-th asking thread's device i mod the
+// device count; nullptr if no device is visible (Finish then reports it).
+inline dlsm_ctx* ThreadContext() {
+  dlsm_ctx* c = nullptr;
+  return dlsm_thread_ctx(&c) == DLSM_OK ? c : nullptr;
+}
+
+// std::allocator's contract over the library's page-locked host pool
+// (dlsm_host_pool_*): a std::vector<uint32_t, PinnedAllocator<uint32_t>> is
+// the reference's hash_entries_ with its storage in DMA-able memory, so
+// Finish's upload of the hashes runs at the link rate instead of through the
+// runtime's pageable staging.  Like operator new under -fno-exceptions, an
+// allocation failure aborts.
+template <class T>
+struct PinnedAllocator {
+  using value_type = T;
+  PinnedAllocator() = default;
+  template <class U>
+  PinnedAllocator(const PinnedAllocator<U>&) {}  // NOLINT
+  T* allocate(size_t n) {
+    void* p = nullptr;
+    uint64_t cap = 0;
+    if (dlsm_host_pool_acquire(n * sizeof(T), &p, &cap) != DLSM_OK || !p) std::abort();
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t) { dlsm_host_pool_release(p); }
+  friend bool operator==(const PinnedAllocator&, const PinnedAllocator&) { return true; }
+  friend bool operator!=(const PinnedAllocator&, const PinnedAllocator&) { return false; }
 };
 
 // Key staging in page-locked host memory: AddKey writes the keys where
@@ -310,8 +344,26 @@ struct BuilderOptions {
 
 class FullFilterBlockBuilder {
  public:
+  // The reference's signature, table/full_filter_block.h:35 --
+  // FullFilterBlockBuilder(ibv_mr* mr, int bloombits_per_key): `mr` is any
+  // memory-region type with `addr` and `length` (ibv_mr binds as-is), the
+  // context is the calling thread's (dlsm_thread_ctx).  AddKey is the
+  // reference's own (full_filter_block.cc:39-49): BloomHash per key into
+  // hash_entries_, a hash equal to the last one dropped; Finish replaces only
+  // the scatter loop (:104-108): hash_entries_ (4 B per distinct key) goes to
+  // the GPU, and the kernels write the filter -- every byte, then the k byte
+  // and Fixed32 line count -- straight into the slot when it is page-locked
+  // (dlsm_host_register the RDMA chunk once), else through staging.
+  template <class MR>
+  FullFilterBlockBuilder(MR* mr, int bits_per_key)
+      : slot_{mr->addr, static_cast<size_t>(mr->length)}, local_mr_(&slot_), bits_per_key_(bits_per_key),
+        num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ThreadContext()), opt_(), keys_(ctx_),
+        reference_addkey_(true), result(static_cast<char*>(mr->addr), 0) {
+    // room for every key the slot's filter can hold: one pool buffer per builder
+    if (bits_per_key > 0) hash_entries_.reserve(static_cast<size_t>(mr->length) * 8u / static_cast<size_t>(bits_per_key) + 64);
+  }
   FullFilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx, BuilderOptions opt = {})
-      : local_mr_(mr), bits_per_key_(bits_per_key),
+      : slot_{nullptr, 0}, local_mr_(mr), bits_per_key_(bits_per_key),
         num_probes_(dlsm_bloom_full_num_probes(bits_per_key)), ctx_(ctx), opt_(opt), keys_(ctx),
         result(static_cast<char*>(mr->addr), 0) {
     if (opt_.hash_in_addkey) pend_bytes_.resize(kHashBlock * 32);  // a block of 20-byte keys fits
@@ -320,13 +372,21 @@ class FullFilterBlockBuilder {
   FullFilterBlockBuilder& operator=(const FullFilterBlockBuilder&) = delete;
 
   // full_filter_block.cc:30-33 -- drops the pending keys.
-  void RestartBlock(uint64_t /*block_offset*/) { clear_keys(); }
+  void RestartBlock(uint64_t /*block_offset*/) {
+    hash_entries_.clear();
+    clear_keys();
+  }
   // full_filter_block.cc:39-49 -- the GPU applies the consecutive-hash dedup.
   // The builder only records the keys (pinned staging) and whether they all
   // have one length (then Finish hands them over as a fixed-stride set: the
   // LDS-tiled key loaders) and whether a key repeats its predecessor (then
   // the line count is counted exactly before bucketing: DLSM_OPT_BUILD_EXACT).
   void AddKey(const Slice& key) {
+    if (reference_addkey_) {  // full_filter_block.cc:39-49, unchanged
+      const uint32_t hash = BloomHash(key.data(), key.size());
+      if (hash_entries_.size() == 0 || hash != hash_entries_.back()) hash_entries_.push_back(hash);
+      return;
+    }
     if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
     if (opt_.hash_in_addkey) {
       // the key joins a small block of pending keys; every kHashBlock keys
@@ -375,6 +435,10 @@ class FullFilterBlockBuilder {
   // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
   // buffer (the slot, or the buffer given to Move_buffer).
   void Finish() {
+    if (reference_addkey_) {
+      finish_hash_entries();
+      return;
+    }
     if (opt_.hash_in_addkey && pend_n_) hash_pending();
     if (stage_status_ != DLSM_OK) {
       status_ = stage_status_;
@@ -403,19 +467,19 @@ class FullFilterBlockBuilder {
     // first (this builder's context belongs to its thread; the caller's
     // setting is restored after the call)
     uint64_t exact = 0;
-    if (dups_ && ctx_) {
+    const bool own_exact = dups_ && !opt_.batcher && ctx_;
+    if (own_exact) {
       dlsm_ctx_get_option(ctx_, DLSM_OPT_BUILD_EXACT, &exact);
       dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, 1);
     }
-    if (opt_.batcher && opt_.hash_in_addkey)
-      status_ = dlsm_batcher_full_build_hashed(opt_.batcher, &job, bits_per_key_, &len);
-    else if (opt_.batcher)  // the batcher's own contexts count exactly when told
-      status_ = dlsm_batcher_full_build(opt_.batcher, &job, bits_per_key_, &len);
+    if (opt_.batcher)  // the flag tells the batcher's executor context to count exactly
+      status_ = dlsm_batcher_submit(opt_.batcher, &job, bits_per_key_,
+                                    (opt_.hash_in_addkey ? DLSM_BATCH_HASHED : 0) | (dups_ ? DLSM_BATCH_EXACT : 0), &len);
     else if (opt_.hash_in_addkey)
       status_ = dlsm_bloom_full_build_hashed(ctx_, &job, 1, bits_per_key_, &len);
     else
       status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
-    if (dups_ && ctx_) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
+    if (own_exact) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
     clear_keys();
     result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
@@ -443,6 +507,23 @@ class FullFilterBlockBuilder {
   int status() const { return status_; }
 
  private:
+  // Finish of the reference-signature form: the filter of hash_entries_
+  // (CalculateSpace + AddHash + trailer, full_filter_block.cc:93-141) built
+  // on the GPU from the 4-byte hashes.
+  void finish_hash_entries() {
+    dlsm_build_job job;
+    job.keys.bytes = reinterpret_cast<const uint8_t*>(hash_entries_.data());
+    job.keys.offsets = nullptr;
+    job.keys.key_len = 4;
+    job.keys.suffix_len = 0;
+    job.keys.n = hash_entries_.size();
+    job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
+    job.out_cap = output_capacity();
+    uint64_t len = 0;
+    status_ = ctx_ ? dlsm_bloom_full_build_hashed(ctx_, &job, 1, bits_per_key_, &len) : DLSM_E_DEVICE;
+    hash_entries_.clear();
+    result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
+  }
   // BloomHash of the pending keys into the staged hashes, dropping a hash
   // equal to its predecessor (full_filter_block.cc:45-48) branch-free: every
   // hash is written, the write position advances only for a kept one.
@@ -504,6 +585,7 @@ class FullFilterBlockBuilder {
     pend_fixed20_ = true;
     stage_status_ = DLSM_OK;
   }
+  FilterSlot slot_;  // the reference-signature form's copy of mr->addr / mr->length
   FilterSlot* local_mr_;
   int bits_per_key_;
   int num_probes_;
@@ -524,6 +606,8 @@ class FullFilterBlockBuilder {
   size_t moved_cap_ = 0;
   int status_ = DLSM_OK;        // the last Finish's result
   int stage_status_ = DLSM_OK;  // key staging of the current table
+  bool reference_addkey_ = false;
+  std::vector<uint32_t, PinnedAllocator<uint32_t>> hash_entries_;  // full_filter_block.h:61
 
  public:
   Slice result;  // Filter data computed so far

@@ -48,7 +48,22 @@ int dlsm_bloom_full_build_hashed(dlsm_ctx*, const dlsm_build_job* j, int n_jobs,
 }
 int dlsm_batcher_full_build(dlsm_batcher*, const dlsm_build_job*, int, uint64_t*) { return DLSM_E_ARG; }
 int dlsm_batcher_full_build_hashed(dlsm_batcher*, const dlsm_build_job*, int, uint64_t*) { return DLSM_E_ARG; }
+int dlsm_batcher_submit(dlsm_batcher*, const dlsm_build_job*, int, int, uint64_t*) { return DLSM_E_ARG; }
+static int g_thread_ctx_token;
+int dlsm_thread_ctx(dlsm_ctx** out) {
+  *out = reinterpret_cast<dlsm_ctx*>(&g_thread_ctx_token);  // only passed to the stubs
+  return DLSM_OK;
 }
+}
+
+// an ibv_mr-shaped region (addr + length among other fields)
+struct MrShaped {
+  void* context;
+  void* pd;
+  void* addr;
+  size_t length;
+  uint32_t handle, lkey, rkey;
+};
 
 #define CHECK(c)                                              \
   do {                                                        \
@@ -60,14 +75,10 @@ int dlsm_batcher_full_build_hashed(dlsm_batcher*, const dlsm_build_job*, int, ui
 
 static uint32_t lcg(uint32_t& x) { return x = x * 1664525u + 1013904223u; }
 
-int main() {
-  std::vector<char> slot(1 << 16);
-  dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
-  dlsm_adapter::BuilderOptions opt;
-  opt.hash_in_addkey = true;
-  dlsm_ctx* fake_ctx = reinterpret_cast<dlsm_ctx*>(&slot);  // only passed to the stubs
-  dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, fake_ctx, opt);
-  int cases = 0;
+// Both forms hand the same hashes over: hash_in_addkey (block hashing) and
+// the reference-signature builder (the reference's per-key AddKey into
+// hash_entries_).
+static int run(dlsm_adapter::FullFilterBlockBuilder& b, int& cases) {
   for (int shape = 0; shape < 6; shape++) {
     for (int n : {0, 1, 15, 16, 17, 255, 256, 257, 4099, 70001}) {
       uint32_t x = 12345u + static_cast<uint32_t>(shape * 1000 + n);
@@ -105,6 +116,26 @@ int main() {
       }
       cases++;
     }
+  }
+  return 0;
+}
+
+int main() {
+  std::vector<char> slot(1 << 16);
+  dlsm_adapter::FilterSlot mr{slot.data(), slot.size()};
+  dlsm_adapter::BuilderOptions opt;
+  opt.hash_in_addkey = true;
+  dlsm_ctx* fake_ctx = reinterpret_cast<dlsm_ctx*>(&slot);  // only passed to the stubs
+  int cases = 0;
+  {
+    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, fake_ctx, opt);
+    if (run(b, cases)) return 1;
+  }
+  {
+    MrShaped ibv{nullptr, nullptr, slot.data(), slot.size(), 0, 0, 0};
+    dlsm_adapter::FullFilterBlockBuilder b(&ibv, 10);
+    if (run(b, cases)) return 1;
+    CHECK(b.result.data() == slot.data());
   }
   std::printf("OK adapter addkey cpu (%d cases, avx512 %d)\n", cases, dlsm_adapter::HasAvx512() ? 1 : 0);
   return 0;

@@ -29,7 +29,84 @@ int orc_filter_block_key_may_match(const uint8_t*, uint64_t, uint64_t, const uin
 
 using dlsm_adapter::Slice;
 
+// <infiniband/verbs.h>'s struct ibv_mr field layout: the reference-signature
+// constructor reads addr and length only, so an ibv_mr binds as-is.
+struct IbvMrShaped {
+  void* context;
+  void* pd;
+  void* addr;
+  size_t length;
+  uint32_t handle, lkey, rkey;
+};
+
+// FullFilterBlockBuilder(ibv_mr* mr, int bloombits_per_key) -- the reference's
+// own signature (table/full_filter_block.h:35) and AddKey
+// (full_filter_block.cc:39-49), the thread's context: every filter byte vs the
+// oracle, in a page-locked slot (kernels store straight into it) and in a
+// pageable one, with repeated keys (the dedup), Move_buffer and Reset.
+static int reference_signature() {
+  void* pinned = nullptr;
+  CHECK(dlsm_host_alloc(256 * 1024, &pinned) == DLSM_OK);
+  std::vector<char> pageable(256 * 1024, 0);
+  for (int slot_kind = 0; slot_kind < 2; slot_kind++) {
+    char* base = slot_kind ? pageable.data() : static_cast<char*>(pinned);
+    IbvMrShaped mr{nullptr, nullptr, base, 256 * 1024, 0, 0, 0};
+    for (int n : {0, 1, 7, 4097, 153846}) {
+      std::memset(base, 0, 256 * 1024);
+      dlsm_adapter::FullFilterBlockBuilder b(&mr, 10);
+      b.RestartBlock(0);
+      std::string flat;
+      std::vector<uint64_t> offs{0};
+      for (int i = 0; i < n; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i / (i % 5 == 0 ? 2 : 1)) * 7 + 3, 20, k);  // runs of repeats
+        b.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+        flat.append(reinterpret_cast<char*>(k), 20);
+        offs.push_back(flat.size());
+      }
+      b.Finish();
+      CHECK(b.status() == DLSM_OK);
+      std::vector<uint8_t> want(256 * 1024, 0);
+      const int64_t wl = orc_full_build(reinterpret_cast<const uint8_t*>(flat.data()), offs.data(), 0, n, 10,
+                                        want.data(), want.size());
+      CHECK(wl > 0 && static_cast<int64_t>(b.result.size()) == wl);
+      CHECK(b.result.data() == base);
+      CHECK(std::memcmp(b.result.data(), want.data(), wl) == 0);
+      // a second table through the same builder after Move_buffer into the slot's back half
+      b.Move_buffer(base + 128 * 1024);
+      b.RestartBlock(0);
+      for (int i = 0; i < 1000; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i) + 99, 20, k);
+        b.AddKey(Slice(reinterpret_cast<char*>(k), 20));
+      }
+      b.Finish();
+      CHECK(b.status() == DLSM_OK && b.result.data() == base + 128 * 1024);
+      std::string f2;
+      std::vector<uint64_t> o2{0};
+      for (int i = 0; i < 1000; i++) {
+        uint8_t k[20];
+        orc_dbbench_key(static_cast<uint64_t>(i) + 99, 20, k);
+        f2.append(reinterpret_cast<char*>(k), 20);
+        o2.push_back(f2.size());
+      }
+      const int64_t w2 = orc_full_build(reinterpret_cast<const uint8_t*>(f2.data()), o2.data(), 0, 1000, 10,
+                                        want.data(), want.size());
+      CHECK(static_cast<int64_t>(b.result.size()) == w2 && std::memcmp(b.result.data(), want.data(), w2) == 0);
+      b.Reset();
+      CHECK(b.result.size() == 0 && b.result.data() == base);
+    }
+  }
+  // the context came from the thread (dlsm_thread_ctx), the same one every time
+  dlsm_ctx* t1 = nullptr;
+  dlsm_ctx* t2 = nullptr;
+  CHECK(dlsm_thread_ctx(&t1) == DLSM_OK && dlsm_thread_ctx(&t2) == DLSM_OK && t1 && t1 == t2);
+  CHECK(dlsm_host_free(pinned) == DLSM_OK);
+  return 0;
+}
+
 int main() {
+  if (reference_signature() != 0) return 1;
   dlsm_ctx* ctx = nullptr;
   CHECK(dlsm_ctx_create(0, &ctx) == DLSM_OK);
   // ---- FullFilterBlockBuilder: the TableBuilder call shape ----

@@ -22,7 +22,16 @@
 //                     threads' concurrent calls become batched builds;
 //       hash       -- one ctx per thread, AddKey hashes on the host (the
 //                     reference's AddKey) and Finish sends 4 B per key;
-//       batch-hash -- both.
+//       batch-hash -- both;
+//       ref        -- the reference's own signature and AddKey: builders
+//                     constructed as FullFilterBlockBuilder(ibv_mr*, bits_per_key)
+//                     (an ibv_mr-shaped region: addr + length), the thread's
+//                     context from dlsm_thread_ctx, AddKey = BloomHash into
+//                     hash_entries_ with the consecutive-duplicate drop
+//                     (full_filter_block.cc:39-49), Finish = the hashed GPU build
+//                     into the page-locked slot.
+// Threads up to 28 = dLSM's 4 flush + 12 compaction + 12 subcompaction
+// builder threads (include/TimberSaw/options.h:73,77-78).
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
@@ -43,6 +52,17 @@ void orc_dbbench_key(uint64_t v, int key_size, uint8_t* out);
 
 using dlsm_adapter::Slice;
 using Clock = std::chrono::steady_clock;
+
+// Field layout of <infiniband/verbs.h>'s struct ibv_mr (context, pd, addr,
+// length, handle, lkey, rkey): the reference-signature constructor reads only
+// addr and length, so the real ibv_mr binds the same way.
+struct IbvMrShaped {
+  void* context;
+  void* pd;
+  void* addr;
+  size_t length;
+  uint32_t handle, lkey, rkey;
+};
 
 class Barrier {
  public:
@@ -79,9 +99,9 @@ struct ThreadResult {
 };
 
 static void run_thread(int t, int threads, int tables, int n, Barrier* bar, ThreadResult* r,
-                       dlsm_adapter::BuilderOptions opt) {
+                       dlsm_adapter::BuilderOptions opt, bool ref) {
   dlsm_ctx* ctx = nullptr;
-  const int ok_ctx = opt.batcher ? DLSM_OK : dlsm_ctx_create(0, &ctx);
+  const int ok_ctx = (opt.batcher || ref) ? DLSM_OK : dlsm_ctx_create(0, &ctx);
   uint64_t spec = 0;
   dlsm_bloom_full_size(n, 10, nullptr, &spec);
   const size_t slot_len = 256 * 1024 > spec ? 256 * 1024 : spec;  // FilterChunk slot (options.h:28)
@@ -99,9 +119,11 @@ static void run_thread(int t, int threads, int tables, int n, Barrier* bar, Thre
     r->what = "ctx_create / host_alloc";
   }
   dlsm_adapter::FilterSlot mr{slot_mem, slot_len};
+  IbvMrShaped ibv{nullptr, nullptr, slot_mem, slot_len, 0, 0, 0};
   auto build = [&](int q, bool timed) {
     if (r->failures) return;
-    dlsm_adapter::FullFilterBlockBuilder b(&mr, 10, ctx, opt);
+    dlsm_adapter::FullFilterBlockBuilder b = ref ? dlsm_adapter::FullFilterBlockBuilder(&ibv, 10)
+                                                 : dlsm_adapter::FullFilterBlockBuilder(&mr, 10, ctx, opt);
     std::memset(slot_mem, 0, slot_len);  // Rep ctor memsets the slot (table_builder_computeside.cc:38)
     const auto t0 = Clock::now();
     b.RestartBlock(0);
@@ -123,6 +145,7 @@ static void run_thread(int t, int threads, int tables, int n, Barrier* bar, Thre
   };
   bar->wait();
   build(0, false);  // warm-up
+  if (ref) dlsm_thread_ctx(&ctx);  // the thread's context the builders took (owned by the library)
   if (!r->failures && ctx) dlsm_ctx_stats(ctx, &r->allocs_after_warmup, nullptr);
   r->gpu_start = bar->wait();
   for (int q = 1; q <= tables; q++) build(q, true);
@@ -142,7 +165,7 @@ static void run_thread(int t, int threads, int tables, int n, Barrier* bar, Thre
     }
   }
   if (slot_mem) dlsm_host_free(slot_mem);
-  if (ctx) dlsm_ctx_destroy(ctx);
+  if (ctx && !ref) dlsm_ctx_destroy(ctx);
 }
 
 int main(int argc, char** argv) {
@@ -160,14 +183,14 @@ int main(int argc, char** argv) {
       return 1;
     }
     opt.batcher = batcher;
-  } else if (mode != "ctx" && mode != "hash") {
+  } else if (mode != "ctx" && mode != "hash" && mode != "ref") {
     std::printf("FAIL unknown mode %s\n", mode.c_str());
     return 1;
   }
   std::vector<ThreadResult> res(threads);
   Barrier bar(threads);
   std::vector<std::thread> th;
-  for (int t = 0; t < threads; t++) th.emplace_back(run_thread, t, threads, tables, n, &bar, &res[t], opt);
+  for (int t = 0; t < threads; t++) th.emplace_back(run_thread, t, threads, tables, n, &bar, &res[t], opt, mode == "ref");
   for (auto& x : th) x.join();
   uint64_t nb = 0, nj = 0, mb = 0;
   if (batcher) {

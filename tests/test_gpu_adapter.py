@@ -120,3 +120,20 @@ def test_concurrent_builders_batched_and_hashed(tmp_path, mode):
     if mode.startswith("batch"):
         assert rec["batches"] >= 1 and rec["max_batch"] >= 1
     print(json.dumps(rec))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads", [16, 28])
+def test_reference_signature_builders(tmp_path, threads):
+    """The reference's own builder signature, FullFilterBlockBuilder(ibv_mr*,
+    bits_per_key), with its own AddKey (BloomHash into hash_entries_) and the
+    thread's context, from 16 and from 28 threads at once (dLSM's 4 flush + 12
+    compaction + 12 subcompaction builders, options.h:73,77-78): every filter
+    equals the oracle's, and no context allocates after its first table."""
+    exe = _compile(tmp_path, "concurrent_builders")
+    out = subprocess.run([str(exe), str(threads), "3", "153846", "ref"], capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0 and "OK concurrent builders" in out.stdout, out.stdout + out.stderr
+    rec = json.loads(out.stdout.splitlines()[0])
+    assert rec["failures"] == 0 and rec["mode"] == "ref" and rec["threads"] == threads
+    print(json.dumps(rec))
