@@ -470,26 +470,67 @@ def run_threads(args) -> int:
             f"[{w.work.lookup_lo}, {w.work.lookup_hi}), overlap {w.overlap}")
     log(f"inputs ready in {time.time() - t_in:.1f}s")
     # the timed steps run from the library's native runner: a std::thread per
-    # device, host barriers around the timed region (dlsm_multi_device_run)
-    elapsed, passes = MG.native_timed_run(workers, args.steps, args.warmup, bpk)
-    w0 = workers[0]
-    build_ms = float(np.mean([b for b, _ in passes]))
-    probe_ms = float(np.mean([p for _, p in passes]))
+    # device, host barriers around the timed region, every device's passes
+    # timed on the sampled steps (dlsm_multi_device_run_timed)
+    elapsed, passes, dev_s = MG.native_timed_run(workers, args.steps, args.warmup, bpk)
+    per_gpu = []
+    for w, ps, ds in zip(workers, passes, dev_s):
+        inp = w.inp
+        per_gpu.append(gpu_share_record(w.rank, w.device, len(inp.tables) * N, inp.lookups.n,
+                                        len(inp.tables) * N * 20 + int(inp.lens.cpu().numpy()[: len(inp.tables)].sum()),
+                                        inp.lookups.n * (20 + inp.fs.mask_bytes) + sum(int(f.numel()) for f in inp.filters),
+                                        ps, ds, args.steps))
+    result = threads_line(args, N_GPU, devices, workers, per_gpu, elapsed, T, N, Q, F, bpk)
+    if not args.no_cpu:
+        # the CPU baseline once, from this process, on the job's first tables
+        # and GPU 0's lookup shard (bounded sample, as at N = 1)
+        order = sorted((s, w, j) for w in workers for j, s in enumerate(w.work.tables))
+        tabs = [w.inp.tables[j] for _, w, j in order]
+        gpu_filters = [w.inp.outs[j][: int(w.inp.lens.cpu().numpy()[j])].cpu().numpy().tobytes() for _, w, j in order]
+        w0 = workers[0]
+        result["cpu_baseline"] = cpu_baseline(args, tabs, gpu_filters, w0.inp.lookups, w0.inp.mask,
+                                              list(w0.inp.filters), N, len(tabs), bpk)
+    print(json.dumps(result), flush=True)
+    for w in workers:
+        w.close()
+    return 0
+
+
+def gpu_share_record(rank, device, build_keys, probe_keys, build_bytes, probe_bytes, passes, device_s, steps):
+    """One GPU's share of the N-GPU job: its sampled pass times (HIP events on
+    its own streams), algorithmic bytes and rates, and its own time over the
+    timed steps."""
+    import numpy as np
+
+    b = float(np.mean([x for x, _ in passes])) if passes else float("nan")
+    p = float(np.mean([y for _, y in passes])) if passes else float("nan")
+    rec = {"gpu": rank, "device": device, "build_keys": build_keys, "probe_keys": probe_keys,
+           "build_ms": round(b, 4), "probe_ms": round(p, 4),
+           "build_alg_GBs": round(build_bytes / (b * 1e-3) / 1e9, 1) if build_keys and b > 0 else None,
+           "probe_alg_GBs": round(probe_bytes / (p * 1e-3) / 1e9, 1) if probe_keys and p > 0 else None,
+           "ms_per_step": round(device_s / steps * 1e3, 4), "sampled_steps": len(passes)}
+    for k in ("build", "probe"):
+        g = rec[k + "_alg_GBs"]
+        rec[k + "_frac"] = round(g / HBM_PEAK_GBS, 4) if g else None
+    return rec
+
+
+def threads_line(args, n_gpu, devices, workers, per_gpu, elapsed, T, N, Q, F, bpk):
+    """The bench line of `--gpus N` (one process, a host thread per GPU): the
+    whole job's rate, every GPU's share (pass times, rates, own step time) and
+    the imbalance between them; the roofline is the dominant pass of the
+    slowest GPU's share."""
     value = (T * N + Q) * args.steps / elapsed / 1e6
-    inp = w0.inp
-    filt_bytes = sum(int(f.numel()) for f in inp.filters)
-    nb = max(1, len(inp.tables) * N)
-    probe_bytes = inp.lookups.n * (20 + inp.fs.mask_bytes) + filt_bytes
-    build_bytes = len(inp.tables) * N * 20 + int(inp.lens.cpu().numpy()[: len(inp.tables)].sum())
-    probe_gbs = probe_bytes / (probe_ms * 1e-3) / 1e9
-    build_gbs = build_bytes / (build_ms * 1e-3) / 1e9
-    dominant = "probe" if probe_ms >= build_ms else "build"
-    ach = probe_gbs if dominant == "probe" else build_gbs
-    result = {
+    slow = max(per_gpu, key=lambda r: r["ms_per_step"])
+    fast = min(per_gpu, key=lambda r: r["ms_per_step"])
+    dominant = "probe" if (slow["probe_ms"] or 0) >= (slow["build_ms"] or 0) else "build"
+    ach = slow[dominant + "_alg_GBs"] or 0.0
+    step_bytes = sum(r["build_keys"] * 21.25 + r["probe_keys"] * 21.16 for r in per_gpu)
+    return {
         "metric": "Bloom build+probe Mkeys/s (device-resident), 20B keys, 10 bits/key",
         "value": round(value, 2),
         "unit": "Mkeys/s",
-        "n_gpus": N_GPU,
+        "n_gpus": n_gpu,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -500,13 +541,13 @@ def run_threads(args) -> int:
         "data": "synthetic db_bench keys (GenerateKeyFromInt), mt19937_64 lookups",
         "config": {
             "workload": (f"build {T} SSTable full filters x {N} keys + probe {Q} lookups vs {F} stacked "
-                         f"filters, split over {N_GPU} GPUs"),
+                         f"filters, split over {n_gpu} GPUs"),
             "key_bytes": 20, "bits_per_key": bpk, "tables": T, "keys_per_table": N,
             "lookups": Q, "filters": F,
-            "parallelism": (f"strong: {T} SSTables split s mod {N_GPU}, filters replicated, {Q} lookups "
-                            f"sharded x{N_GPU}; one process, one host thread + context + stream per GPU"),
-            "launch": "threads (dlsm_multi_device_run)",
-            "pass_events_every": MG.event_stride(args.steps),
+            "parallelism": (f"strong: {T} SSTables split s mod {n_gpu}, filters replicated, {Q} lookups "
+                            f"sharded x{n_gpu}; one process, one host thread + context + stream per GPU"),
+            "launch": "threads (dlsm_multi_device_run_timed)",
+            "pass_events_every": event_stride_of(args.steps),
             "devices": devices,
             "rehearsal": bool(args.rehearse),
             "gpu_tables": [w.work.tables for w in workers],
@@ -516,21 +557,27 @@ def run_threads(args) -> int:
             "probe_chunk_lg": args.probe_chunk_lg, "probe_slice_lg": args.probe_slice_lg,
         },
         "roofline": {
-            "bound": "hbm", "kernel": f"{dominant} pass (GPU 0's share)", "achieved": round(ach, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+            "bound": "hbm", "kernel": f"{dominant} pass of the slowest GPU's share (gpu {slow['gpu']})",
+            "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
             "traffic": None,
-            **pass_timing_note(w0.overlap, MG.event_stride(args.steps)),
-            **step_roofline(probe_bytes + build_bytes, elapsed / args.steps),
+            "traffic_note": "PMC traffic is committed for the one-GPU job only (profiles/traffic.json)",
+            **pass_timing_note(any(w.overlap for w in workers), event_stride_of(args.steps)),
+            **step_roofline(step_bytes, elapsed / args.steps),
         },
-        "build": {"ms": round(build_ms, 4), "mkeys_s": round(nb / build_ms / 1e3, 1),
-                  "alg_GBs": round(build_gbs, 1), "alg_bytes_per_key": round(build_bytes / nb, 3)},
-        "probe": {"ms": round(probe_ms, 4), "mkeys_s": round(max(1, inp.lookups.n) / probe_ms / 1e3, 1),
-                  "alg_GBs": round(probe_gbs, 1), "alg_bytes_per_key": round(probe_bytes / max(1, inp.lookups.n), 3)},
+        "per_gpu": per_gpu,
+        "imbalance": {"slowest_gpu": slow["gpu"], "fastest_gpu": fast["gpu"],
+                      "max_over_min_ms_per_step": round(slow["ms_per_step"] / fast["ms_per_step"], 4)
+                      if fast["ms_per_step"] > 0 else None,
+                      "max_minus_min_ms_per_step": round(slow["ms_per_step"] - fast["ms_per_step"], 4)},
+        "build": {"ms": slow["build_ms"], "note": "slowest GPU's share; per_gpu has every GPU"},
+        "probe": {"ms": slow["probe_ms"], "note": "slowest GPU's share; per_gpu has every GPU"},
     }
-    print(json.dumps(result), flush=True)
-    for w in workers:
-        w.close()
-    return 0
+
+
+def event_stride_of(steps):
+    from dlsm_amd.multigpu import event_stride
+
+    return event_stride(steps)
 
 
 def load_traffic(path, config, dominant):

@@ -140,6 +140,9 @@ SIGNATURES = [
                                        C.POINTER(C.c_double), C.POINTER(C.c_float)]),
     ("dlsm_multi_device_run_sampled", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
                                                C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float)]),
+    ("dlsm_multi_device_run_timed", C.c_int, [C.POINTER(dlsm_device_work), C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float),
+                                             C.POINTER(C.c_double)]),
 ]
 
 _LIB = None

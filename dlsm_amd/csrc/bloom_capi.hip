@@ -161,9 +161,16 @@ struct dlsm_ctx {
   // descriptors): a ring of slots, each reused only after the event recorded
   // behind its copy has completed -- a pageable (e.g. stack) source could be
   // gone before a queued copy reads it.
+  // The slots are carved from one page-locked block allocated with the
+  // context (hipHostMalloc takes a process-wide lock and milliseconds: lazily
+  // allocated slots stalled concurrent builder threads' first calls by up to
+  // 15 ms); a table larger than a slot gets a buffer of its own.
   static constexpr int kUpSlots = 16;
+  static constexpr uint64_t kUpSlotBytes = 16384;
+  uint8_t* up_block = nullptr;
   uint8_t* up_buf[kUpSlots] = {};
   uint64_t up_cap[kUpSlots] = {};
+  bool up_own[kUpSlots] = {};  // up_buf[i] is a buffer of its own (not in up_block)
   hipEvent_t up_ev[kUpSlots] = {};
   bool up_live[kUpSlots] = {};
   int up_next = 0;
@@ -346,15 +353,16 @@ int ctx_upload(dlsm_ctx* ctx, void* dst, const void* src, size_t n, hipStream_t 
     DLSM_TRY(hipEventSynchronize(ctx->up_ev[i]));
     ctx->up_live[i] = false;
   }
-  if (!ctx->up_ev[i]) DLSM_TRY(hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming));
   if (ctx->up_cap[i] < n) {
-    if (ctx->up_buf[i]) (void)hipHostFree(ctx->up_buf[i]);
+    if (ctx->up_own[i]) (void)hipHostFree(ctx->up_buf[i]);
     ctx->up_buf[i] = nullptr;
     ctx->up_cap[i] = 0;
-    uint64_t c = 4096;
+    ctx->up_own[i] = false;
+    uint64_t c = 2 * dlsm_ctx::kUpSlotBytes;
     while (c < n) c <<= 1;
     DLSM_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->up_buf[i]), c, hipHostMallocDefault));
     ctx->up_cap[i] = c;
+    ctx->up_own[i] = true;
   }
   memcpy(ctx->up_buf[i], src, n);
   DLSM_TRY(hipMemcpyAsync(dst, ctx->up_buf[i], n, hipMemcpyHostToDevice, s));
@@ -484,6 +492,14 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
     e = hipEventCreateWithFlags(&ctx->ev_part[b], hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_free[b], hipEventDisableTiming);
   }
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&ctx->up_block), dlsm_ctx::kUpSlots * dlsm_ctx::kUpSlotBytes,
+                      hipHostMallocDefault);
+  for (int i = 0; i < dlsm_ctx::kUpSlots && e == hipSuccess; i++) {
+    ctx->up_buf[i] = ctx->up_block + i * dlsm_ctx::kUpSlotBytes;
+    ctx->up_cap[i] = dlsm_ctx::kUpSlotBytes;
+    e = hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming);
+  }
   ctx->stream = ctx->own;
   if (e != hipSuccess) {
     dlsm_ctx_destroy(ctx);
@@ -542,9 +558,10 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   if (ctx->h_out) (void)hipHostFree(ctx->h_out);
   if (ctx->h_len) (void)hipHostFree(ctx->h_len);
   for (int i = 0; i < dlsm_ctx::kUpSlots; i++) {
-    if (ctx->up_buf[i]) (void)hipHostFree(ctx->up_buf[i]);
+    if (ctx->up_own[i]) (void)hipHostFree(ctx->up_buf[i]);
     if (ctx->up_ev[i]) (void)hipEventDestroy(ctx->up_ev[i]);
   }
+  if (ctx->up_block) (void)hipHostFree(ctx->up_block);
   delete ctx;
   return DLSM_OK;
 }

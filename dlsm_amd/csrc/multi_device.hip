@@ -60,8 +60,9 @@ int drain(const dlsm_device_work& w) {
 
 }  // namespace
 
-extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n, int bits_per_key, int steps,
-                                             int warmup, int event_every, double* wall_seconds, float* pass_ms) {
+extern "C" int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n, int bits_per_key, int steps,
+                                           int warmup, int event_every, double* wall_seconds, float* pass_ms,
+                                           double* device_seconds) {
   if (!work || n < 1 || steps < 1 || warmup < 0 || !wall_seconds || event_every < 1) return DLSM_E_ARG;
   for (int d = 0; d < n; d++) {
     const dlsm_device_work& w = work[d];
@@ -79,14 +80,15 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
       if (hipSetDevice(dlsm_ctx_device(w.probe_ctx)) != hipSuccess) st = DLSM_E_DEVICE;
       for (int i = 0; i < warmup && st == DLSM_OK; i++) st = step(w, bits_per_key);
       if (st == DLSM_OK) st = drain(w);
-      // Device 0 brackets each pass of every event_every-th step with events
-      // on the stream it runs on (an event pair at a call boundary leaves the
-      // GPU idle for several microseconds: profiles/r03_o_pass_events_ab.txt).
-      // With the build on a stream of its own, a sampled step runs its passes
-      // alone -- its build after the probes before it, its probe after its
-      // build, the next build after its probe -- so the events time each pass
-      // by itself (the roofline's kernel time), not beside the other.
-      const bool events = d == 0 && pass_ms && st == DLSM_OK;
+      // Every device brackets each pass of every event_every-th step with
+      // events on the stream it runs on (an event pair at a call boundary
+      // leaves the GPU idle for several microseconds:
+      // profiles/r03_o_pass_events_ab.txt).  With the build on a stream of
+      // its own, a sampled step runs its passes alone -- its build after the
+      // probes before it, its probe after its build, the next build after its
+      // probe -- so the events time each pass by itself (the roofline's
+      // kernel time), not beside the other.
+      const bool events = pass_ms && st == DLSM_OK;
       std::vector<hipEvent_t> ev;
       hipEvent_t gate = nullptr;
       if (events) {
@@ -100,6 +102,7 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
       hipStream_t ps = static_cast<hipStream_t>(dlsm_ctx_stream(w.probe_ctx));
       const bool two = bs != ps;
       start.wait();  // every device idle; the host clock starts
+      const auto td = std::chrono::steady_clock::now();
       for (int i = 0; i < steps && st == DLSM_OK; i++) {
         const bool e = sampled(i);
         if (e) {
@@ -122,16 +125,20 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
         }
       }
       if (st == DLSM_OK) st = drain(w);
+      // this device's own time: from the start barrier to its drain
+      if (device_seconds)
+        device_seconds[d] = std::chrono::duration<double>(std::chrono::steady_clock::now() - td).count();
       end.wait();  // every device drained; the host clock stops
       if (events) {
+        float* pm = pass_ms + 2 * static_cast<size_t>(steps) * d;
         for (int i = 0; i < steps; i++) {
           float b = -1.f, p = -1.f;  // not sampled
           if (sampled(i) && st == DLSM_OK &&
               (hipEventElapsedTime(&b, ev[4 * i + 0], ev[4 * i + 1]) != hipSuccess ||
                hipEventElapsedTime(&p, ev[4 * i + 2], ev[4 * i + 3]) != hipSuccess))
             st = DLSM_E_DEVICE;
-          pass_ms[2 * i] = b;
-          pass_ms[2 * i + 1] = p;
+          pm[2 * i] = b;
+          pm[2 * i + 1] = p;
         }
         for (auto& e : ev) (void)hipEventDestroy(e);
         if (gate) (void)hipEventDestroy(gate);
@@ -147,6 +154,17 @@ extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n
   for (int s : status)
     if (s != DLSM_OK) return s;
   return DLSM_OK;
+}
+
+extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n, int bits_per_key, int steps,
+                                             int warmup, int event_every, double* wall_seconds, float* pass_ms) {
+  if (n < 1 || steps < 1) return DLSM_E_ARG;
+  std::vector<float> all(pass_ms ? 2 * static_cast<size_t>(steps) * n : 0);
+  const int st = dlsm_multi_device_run_timed(work, n, bits_per_key, steps, warmup, event_every, wall_seconds,
+                                             pass_ms ? all.data() : nullptr, nullptr);
+  if (pass_ms && st == DLSM_OK)
+    for (int i = 0; i < 2 * steps; i++) pass_ms[i] = all[i];  // device 0's
+  return st;
 }
 
 extern "C" int dlsm_multi_device_run(const dlsm_device_work* work, int n, int bits_per_key, int steps, int warmup,

@@ -286,29 +286,38 @@ def event_stride(steps: int, samples: int = PASS_EVENT_SAMPLES) -> int:
     return max(1, steps // max(1, samples))
 
 
-def native_run(works, steps: int, warmup: int, bits_per_key: int, event_every: int | None = None):
-    """dlsm_multi_device_run_sampled over dlsm_device_work structs: (seconds,
-    [(build_ms, probe_ms) per sampled step] of the first device)."""
+def native_run(works, steps: int, warmup: int, bits_per_key: int, event_every: int | None = None,
+               per_device: bool = False):
+    """dlsm_multi_device_run_timed over dlsm_device_work structs: (seconds,
+    [(build_ms, probe_ms) per sampled step] of the first device), or with
+    per_device (seconds, [that list per device], [each device's own seconds])."""
     import ctypes as C
 
     from . import _lib as L
     from . import check, lib
 
+    n = len(works)
     every = event_stride(steps) if event_every is None else event_every
-    arr = (L.dlsm_device_work * len(works))(*works)
+    arr = (L.dlsm_device_work * n)(*works)
     wall = C.c_double(0.0)
-    pm = (C.c_float * (2 * steps))()
-    check(lib().dlsm_multi_device_run_sampled(arr, len(works), bits_per_key, steps, warmup, every, C.byref(wall),
-                                              pm), "multi_device_run")
-    return wall.value, [(pm[2 * i], pm[2 * i + 1]) for i in range(steps) if pm[2 * i + 1] >= 0]
+    pm = (C.c_float * (2 * steps * n))()
+    ds = (C.c_double * n)()
+    check(lib().dlsm_multi_device_run_timed(arr, n, bits_per_key, steps, warmup, every, C.byref(wall), pm, ds),
+          "multi_device_run")
+    passes = [[(pm[2 * steps * d + 2 * i], pm[2 * steps * d + 2 * i + 1]) for i in range(steps)
+               if pm[2 * steps * d + 2 * i + 1] >= 0] for d in range(n)]
+    if per_device:
+        return wall.value, passes, [ds[d] for d in range(n)]
+    return wall.value, passes[0]
 
 
 def native_timed_run(workers, steps: int, warmup: int, bits_per_key: int):
     """The timed region run by the library's native runner
-    (dlsm_multi_device_run: a std::thread per device, host barriers on both
-    sides of the timed steps, device 0's passes timed with HIP events).
-    Returns (seconds, [(build_ms, probe_ms) per step] of device 0)."""
-    return native_run([w.device_work() for w in workers], steps, warmup, bits_per_key)
+    (dlsm_multi_device_run_timed: a std::thread per device, host barriers on
+    both sides of the timed steps, every device's passes timed with HIP events
+    on the sampled steps).  Returns (seconds, [(build_ms, probe_ms) per sampled
+    step] per device, [each device's own seconds])."""
+    return native_run([w.device_work() for w in workers], steps, warmup, bits_per_key, per_device=True)
 
 
 def build_workers(n_gpus: int, devices: list, T: int, N: int, Q: int, F: int, bpk: int,

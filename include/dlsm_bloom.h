@@ -481,6 +481,15 @@ int dlsm_multi_device_run(const dlsm_device_work* work, int n_devices, int bits_
  * pass_ms holds each pass's own time rather than its time beside the other. */
 int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps,
                                   int warmup, int event_every, double* wall_seconds, float* pass_ms);
+/* The same, with every entry's passes timed: pass_ms (host float[n_devices *
+ * 2 * steps], or NULL) holds entry d's build / probe ms of step i at
+ * [d * 2 * steps + 2 * i] / [+ 1] (-1 on the steps not sampled), and
+ * device_seconds (host double[n_devices], or NULL) each entry's own time from
+ * the start barrier until its device drained -- the slowest is the wall time,
+ * the spread the N-GPU job's imbalance. */
+int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n_devices, int bits_per_key, int steps,
+                                int warmup, int event_every, double* wall_seconds, float* pass_ms,
+                                double* device_seconds);
 
 /* ---- measurement helper (not on the filter path) ------------------------ */
 

@@ -387,6 +387,24 @@ class FullFilterBlockBuilder {
       if (hash_entries_.size() == 0 || hash != hash_entries_.back()) hash_entries_.push_back(hash);
       return;
     }
+    if (opt_.hash_in_addkey && key.size() == 20 && pend_fixed20_ && stage_status_ == DLSM_OK) {
+      // db_bench's shape: the key joins the pending block (two fixed-size copies)
+      char* d = pend_bytes_.data() + pend_size_;
+      std::memcpy(d, key.data(), 16);
+      std::memcpy(d + 16, key.data() + 16, 4);
+      pend_size_ += 20;
+      if (++pend_n_ == kHashBlock) hash_pending();
+      return;
+    }
+    add_key_staged(key);  // kept out of line: AddKey itself stays small enough to inline
+  }
+  // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
+  // buffer (the slot, or the buffer given to Move_buffer).
+  void Finish() { finish_impl(); }
+  void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
+
+ private:
+  __attribute__((noinline)) void add_key_staged(const Slice& key) {
     if (stage_status_ != DLSM_OK) return;  // staging failed: Finish reports it
     if (opt_.hash_in_addkey) {
       // the key joins a small block of pending keys; every kHashBlock keys
@@ -432,9 +450,7 @@ class FullFilterBlockBuilder {
     last_len_ = key.size();
     n_++;
   }
-  // full_filter_block.cc:93-141 -- writes the filter into result.data()'s
-  // buffer (the slot, or the buffer given to Move_buffer).
-  void Finish() {
+  void finish_impl() {
     if (reference_addkey_) {
       finish_hash_entries();
       return;
@@ -483,7 +499,8 @@ class FullFilterBlockBuilder {
     clear_keys();
     result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
-  void Reset() { result.Reset(static_cast<char*>(local_mr_->addr), 0); }
+
+ public:
   // Output goes to p from now on (full_filter_block.cc:144-146).  Every
   // reference caller moves back into its own slot (local_filter_mr[0]->addr:
   // table_builder_computeside.cc:566, table_builder_bacs.cpp:553,

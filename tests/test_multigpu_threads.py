@@ -98,8 +98,11 @@ def test_two_logical_devices_strong_scaling_parity(orc):
             w.inp.mask.zero_()
             for o in w.inp.outs:
                 o.zero_()
-        dt, passes = MG.native_timed_run(workers, steps=2, warmup=1, bits_per_key=10)
-        assert dt > 0 and len(passes) == 2 and all(b > 0 and p > 0 for b, p in passes)
+        dt, passes, dev_s = MG.native_timed_run(workers, steps=2, warmup=1, bits_per_key=10)
+        # every device's sampled passes are timed, and each device's own time is at most the wall time
+        assert dt > 0 and len(passes) == 2 and all(len(p) == 2 for p in passes)
+        assert all(b > 0 and p > 0 for d in passes for b, p in d)
+        assert len(dev_s) == 2 and all(0 < x <= dt * 1.001 for x in dev_s)
         assert [w.work.tables for w in workers] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
         assert [(w.work.lookup_lo, w.work.lookup_hi) for w in workers] == [(0, _Q // 2), (_Q // 2, _Q)]
         union = {}
