@@ -6,7 +6,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
 SRC := dlsm_amd/csrc/bloom_kernels.hip dlsm_amd/csrc/bloom_capi.hip dlsm_amd/csrc/block_crc.hip \
        dlsm_amd/csrc/key_select.hip dlsm_amd/csrc/stream_probe.hip \
-       dlsm_amd/csrc/multi_device.hip dlsm_amd/csrc/batcher.hip
+       dlsm_amd/csrc/multi_device.hip dlsm_amd/csrc/batcher.hip dlsm_amd/csrc/host_hash.hip
 HDR := dlsm_amd/csrc/bloom_math.h dlsm_amd/csrc/bloom_internal.h include/dlsm_bloom.h
 LIB := dlsm_amd/lib/libdlsm_bloom.so
 OBJ := $(patsubst dlsm_amd/csrc/%.hip,build/%.o,$(SRC))

@@ -404,6 +404,9 @@ def main():
     # ---- host-inclusive (PCIe) rate, N=1 only: recorded, never `value` ----
     if world == 1 and not args.no_e2e:
         result["e2e"] = e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev)
+        L = lens.cpu().numpy()
+        ref = ([outs[s][: int(L[s])].cpu().numpy().tobytes() for s in range(len(tables))], mask.cpu().numpy())
+        result["e2e_hashed"] = e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref)
         # the same build with the job table changing every call (a flush
         # stream hands over new tables each time: the upload is paid)
         result["build"]["rotating_batches_ms"] = round(rotating_build_ms(ctx, stream, tables, outs, lens, bpk), 4)
@@ -421,7 +424,9 @@ def main():
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if world == 1 and rank == 0 and not args.no_cpu:
         filters = [f for f in inp.filters]
-        result["cpu_baseline"] = cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk,
+        L = lens.cpu().numpy()
+        gpu_filters = [outs[s][: int(L[s])].cpu().numpy().tobytes() for s in range(T)]
+        result["cpu_baseline"] = cpu_baseline(args, tables, gpu_filters, qk, mask, filters, N, T, bpk,
                                               legacy_out=legacy_out)
 
     if rank == 0:
@@ -665,6 +670,97 @@ def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):
             "note": "H2D keys + build + probe + D2H filters/masks, pinned host buffers"}
 
 
+def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_500_000, reps=3):
+    """Host-inclusive rate with the hashing on the host, as the reference does
+    it (BloomHash in AddKey and in KeyMayMatch, full_filter_block.cc:45,271):
+    keys start in pinned host memory, the host's cores hash them
+    (dlsm_bloom_hash_batch, inside the timed region), 4 B per key go H2D, the
+    GPU builds from the hashes (dlsm_bloom_full_build_hashed_dev) and probes
+    from them (dlsm_bloom_full_probe_hashed_dev), filters and masks come back
+    D2H into pinned memory.  The job is cut into chunks (the build's tables,
+    then lookup chunks) over two pinned hash buffers, so the host hashes chunk
+    i + 1 while chunk i's H2D copy and kernels run; the D2H copies run on a
+    second stream (PCIe is full duplex).  `ref` = (filters, mask) of the
+    device-resident run: the outputs are checked against them."""
+    import numpy as np
+    import torch
+
+    import dlsm_amd
+
+    T, N, Q = len(tables), tables[0].n, qk.n
+    mb = fs.mask_bytes
+    h_tabs = [t.data.cpu().pin_memory() for t in tables]
+    h_q = qk.data.cpu().pin_memory()
+    cap = max(T * N, chunk_keys)
+    hb = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(2)]
+    hb_np = [h.numpy() for h in hb]
+    db = [torch.empty(cap, dtype=torch.int32, device=dev) for _ in range(2)]
+    outs = [torch.zeros(dlsm_amd.full_size(t.n, bpk)[0] + 16, dtype=torch.uint8, device=dev) for t in tables]
+    lens = torch.zeros(T, dtype=torch.uint64, device=dev)
+    h_outs = [torch.empty_like(o, device="cpu").pin_memory() for o in outs]
+    h_lens = torch.empty(T, dtype=torch.uint64).pin_memory()
+    mask = torch.empty(Q * mb, dtype=torch.uint8, device=dev)
+    h_mask = torch.empty(Q * mb, dtype=torch.uint8).pin_memory()
+    s_out = torch.cuda.Stream(device=dev)
+    tab_np = [h.numpy() for h in h_tabs]
+    q_np = h_q.numpy()
+    chunks = [("build", 0, T * N)] + [("probe", lo, min(Q, lo + chunk_keys)) for lo in range(0, Q, chunk_keys)]
+
+    def one_step():
+        free = [None, None]
+        for i, (kind, lo, hi) in enumerate(chunks):
+            b = i % 2
+            if free[b] is not None:
+                free[b].synchronize()  # the H2D that last read this staging buffer
+            n = hi - lo
+            if kind == "build":
+                for s_, t in enumerate(tables):
+                    dlsm_amd.hash_batch(dlsm_amd.Keys(tab_np[s_], t.n, 20), out=hb_np[b][s_ * N:(s_ + 1) * N])
+            else:
+                dlsm_amd.hash_batch(dlsm_amd.Keys(q_np[lo * 20:hi * 20], n, 20), out=hb_np[b][:n])
+            with torch.cuda.stream(stream):
+                db[b][:n].copy_(hb[b][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            free[b] = ev
+            if kind == "build":
+                ctx.full_build_hashed_dev([db[b][s_ * N:(s_ + 1) * N] for s_ in range(T)], outs, lens, bpk)
+            else:
+                ctx.full_probe_hashed_dev(fs, db[b][:n], mask[lo * mb:hi * mb], n)
+            done = torch.cuda.Event()
+            done.record(stream)
+            s_out.wait_event(done)
+            with torch.cuda.stream(s_out):
+                if kind == "build":
+                    for h, o in zip(h_outs, outs):
+                        h.copy_(o, non_blocking=True)
+                    h_lens.copy_(lens, non_blocking=True)
+                else:
+                    h_mask[lo * mb:hi * mb].copy_(mask[lo * mb:hi * mb], non_blocking=True)
+        stream.synchronize()
+        s_out.synchronize()
+
+    one_step()  # warm-up (workspaces, pool threads)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        one_step()
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    L = h_lens.numpy()
+    ref_filters, ref_mask = ref
+    ok = (all(h_outs[s_][: int(L[s_])].numpy().tobytes() == ref_filters[s_] for s_ in range(T))
+          and bool(np.array_equal(h_mask.numpy(), ref_mask)))
+    nk = T * N + Q
+    return {"mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
+            "ms_per_step_reps": [round(x * 1e3, 3) for x in times],
+            "host_hash_threads": "all usable cores (dlsm_bloom_hash_batch pool)",
+            "chunk_keys": chunk_keys, "h2d_bytes_per_key": 4,
+            "matches_device_resident": ok,
+            "note": ("host BloomHash (timed) + H2D 4 B/key hashes + hashed build / probe + D2H filters/masks, "
+                     "chunked, pinned host buffers")}
+
+
 def host_cores() -> int:
     """Host cores this process may use: the CPU affinity set, capped by a
     cgroup CPU quota when one is set (a GPU box's share of its host)."""
@@ -678,7 +774,7 @@ def host_cores() -> int:
     return max(1, n)
 
 
-def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk, legacy_out=None):
+def cpu_baseline(args, tables, gpu_filters, qk, mask, filters, N, T, bpk, legacy_out=None):
     """The CPU path timed on this box's host cores on a bounded sample of the
     bench workload, at T = 1 and T = all cores: the reference's own code
     (oracle/_ref/libref.so, built in place from /root/reference, when it
@@ -696,8 +792,6 @@ def cpu_baseline(args, tables, outs, lens, qk, mask, filters, N, T, bpk, legacy_
     nq = min(args.cpu_probe_sample, qk.n)
     n1 = min(1_000_000, nq)
     h_q = qk.data[: nq * 20].cpu().numpy()
-    L = lens.cpu().numpy()
-    gpu_filters = [outs[s][: int(L[s])].cpu().numpy().tobytes() for s in range(T)]
     gpu_mask = mask[:nq].cpu().numpy()
     kind = "reference" if oracle.ref_lib() is not None else "port"
     one = oracle.timed_cpu_baseline(kind, h_tabs[:1], N, h_filters, h_q[: n1 * 20], n1, bpk, 1)

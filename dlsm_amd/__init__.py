@@ -99,6 +99,17 @@ def crc32c(data: bytes, init: int = 0) -> int:
     return int(lib().dlsm_crc32c_extend(init, b, len(data)))
 
 
+def hash_batch(keys: "Keys", out: Optional[np.ndarray] = None, threads: int = 0) -> np.ndarray:
+    """BloomHash of every key of a host key set on the host's cores
+    (dlsm_bloom_hash_batch): uint32[n], numpy or a pinned torch CPU tensor's
+    storage passed as ``out``."""
+    if out is None:
+        out = np.empty(max(keys.n, 1), dtype=np.uint32)
+    ks = keys.c()
+    check(lib().dlsm_bloom_hash_batch(C.byref(ks), _ptr(out), threads), "hash_batch")
+    return out[: keys.n] if isinstance(out, np.ndarray) else out
+
+
 def crc32c_mask(crc: int) -> int:
     return int(lib().dlsm_crc32c_mask(crc))
 
@@ -499,6 +510,13 @@ class Context:
         ks = keys.c()
         check(lib().dlsm_bloom_full_probe(self.h, fs.h, C.byref(ks), mask.ctypes.data), "full_probe")
         return mask[: keys.n * fs.mask_bytes]
+
+    def full_probe_hashed_dev(self, fs: FilterSet, hashes, mask, n: Optional[int] = None):
+        """Probe from BloomHash values (device uint32 tensor); asynchronous."""
+        n = int(hashes.numel()) if n is None else n
+        ks = Keys(hashes, n, 4).c()
+        check(lib().dlsm_bloom_full_probe_hashed_dev(self.h, fs.h, C.byref(ks), _ptr(mask)),
+              "full_probe_hashed_dev")
 
     def full_probe_dev(self, fs: FilterSet, keys: Keys, mask):
         ks = keys.c()

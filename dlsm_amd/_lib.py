@@ -122,6 +122,8 @@ SIGNATURES = [
     ("dlsm_version_slots", C.c_int, [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("dlsm_version_probe_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), C.c_uint64, _VP, _VP]),
     ("dlsm_bloom_full_probe", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_full_probe_hashed_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
+    ("dlsm_bloom_hash_batch", C.c_int, [C.POINTER(dlsm_keyset), _VP, C.c_int]),
     ("dlsm_bloom_legacy_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),

@@ -1560,14 +1560,16 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   const uint64_t C = 1ull << lgC;
   const int mb = (fs->F + 7) / 8;
   const uint32_t nC = ceil_div_u32(n, C);
-  DLSM_CHECK(ctx->hashes.ensure(n));
-  DLSM_TRY(launch_probe_hash(kd, ctx->hashes.p, mode, s));
-  KeyDesc hk{};
-  hk.bytes = reinterpret_cast<const uint8_t*>(ctx->hashes.p);
-  hk.offsets = nullptr;
-  hk.n = n;
-  hk.key_len = 4;
-  hk.suffix = 0;
+  KeyDesc hk = kd;  // hashed lookups (KM_HASH) are probed as given
+  if (mode != KM_HASH) {
+    DLSM_CHECK(ctx->hashes.ensure(n));
+    DLSM_TRY(launch_probe_hash(kd, ctx->hashes.p, mode, s));
+    hk.bytes = reinterpret_cast<const uint8_t*>(ctx->hashes.p);
+    hk.offsets = nullptr;
+    hk.n = n;
+    hk.key_len = 4;
+    hk.suffix = 0;
+  }
   uint32_t Smax = 0;
   for (const auto& g : fs->groups) {
     int lg;
@@ -1601,16 +1603,20 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
 
 }  // namespace
 
-int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
-                              uint8_t* mask_dev) {
+namespace {
+// hashed: the keys are BloomHash values (u32 each, key_len 4), as the host
+// computes them in KeyMayMatch (full_filter_block.cc:271).
+int full_probe_dev_impl(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys, uint8_t* mask_dev,
+                        bool hashed) {
   if (!ctx || !fs || !keys) return DLSM_E_ARG;
   if (fs->device != ctx->device) return DLSM_E_ARG;
   DLSM_CHECK(validate_keyset(*keys));
+  if (hashed && !is_hash_set(*keys)) return DLSM_E_ARG;
   if (keys->n == 0) return DLSM_OK;
   if (!mask_dev) return DLSM_E_ARG;
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
-  const int mode = is_k20(*keys) ? KM_K20 : (is_k28(*keys) ? KM_K28 : KM_GENERIC);
+  const int mode = hashed ? KM_HASH : is_k20(*keys) ? KM_K20 : (is_k28(*keys) ? KM_K28 : KM_GENERIC);
   const KeyDesc kd = to_desc(*keys);
   const int lgC = ctx->probe_lgc;
   const uint64_t C = 1ull << lgC;
@@ -1686,6 +1692,17 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
     if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
   }
   return DLSM_OK;
+}
+}  // namespace
+
+int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
+                              uint8_t* mask_dev) {
+  return full_probe_dev_impl(ctx, fs, keys, mask_dev, false);
+}
+
+int dlsm_bloom_full_probe_hashed_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* hashes,
+                                     uint8_t* mask_dev) {
+  return full_probe_dev_impl(ctx, fs, hashes, mask_dev, true);
 }
 
 int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,

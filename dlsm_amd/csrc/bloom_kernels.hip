@@ -2120,6 +2120,8 @@ hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys,
   const unsigned g = grid_for(keys.n, 256u * 64u);
   if (mode == KM_K20)
     probe_direct_kernel<KM_K20><<<g, kBlock, 0, s>>>(fs, n_filters, keys, mask);
+  else if (mode == KM_HASH)
+    probe_direct_kernel<KM_HASH><<<g, kBlock, 0, s>>>(fs, n_filters, keys, mask);
   else
     probe_direct_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(fs, n_filters, keys, mask);
   return hipGetLastError();

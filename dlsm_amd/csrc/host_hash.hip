@@ -1,0 +1,217 @@
+// dlsm_amd/csrc/host_hash.hip -- BloomHash of a batch of host keys on the
+// host's cores (host code only; no device work).
+//
+// The reference hashes on the host: FullFilterBlockBuilder::AddKey
+// (table/full_filter_block.cc:45) and FullFilterBlockReader::KeyMayMatch
+// (:271) call BloomHash (include/TimberSaw/filter_policy.h:26-28,
+// util/hash.cc:22-62) per key.  A caller whose keys live in host memory
+// (memtable / compaction iterators, Get() callers) can hash them here and
+// hand the GPU 4 bytes per key (dlsm_bloom_full_build_hashed*,
+// dlsm_bloom_full_probe_hashed_dev) instead of the key bytes: a quarter of
+// the PCIe traffic for 20-byte keys.  Sixteen 20-byte keys at a time with
+// AVX-512 when the CPU has it, on a process-wide pool of host threads.
+#include <hip/hip_runtime.h>  // bloom_math.h's host/device qualifiers
+
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+#include "../../include/dlsm_bloom.h"
+#include "bloom_math.h"
+
+namespace {
+
+using dlsm::bloom_hash_host;
+using dlsm::hash_init;
+using dlsm::hash_word;
+using dlsm::kBloomSeed;
+using dlsm::kHashM;
+
+// Sixteen 20-byte keys at p .. p + 300 (util/hash.cc's five rounds on all
+// sixteen at once): the 80 dwords load as five vectors, dword j of key q
+// (5q + j) is gathered across them with two-source permutes.
+#if defined(__x86_64__)
+__attribute__((target("avx512f"))) void hash20x16_avx512(const uint8_t* p, uint32_t* out) {
+  const __m512i v0 = _mm512_loadu_si512(p), v1 = _mm512_loadu_si512(p + 64), v2 = _mm512_loadu_si512(p + 128),
+                v3 = _mm512_loadu_si512(p + 192), v4 = _mm512_loadu_si512(p + 256);
+  const __m512i q5 = _mm512_mullo_epi32(_mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15),
+                                        _mm512_set1_epi32(5));
+  const __m512i m = _mm512_set1_epi32(static_cast<int>(kHashM));
+  __m512i h = _mm512_set1_epi32(static_cast<int>(hash_init(20, kBloomSeed)));
+  for (int j = 0; j < 5; j++) {
+    const __m512i d = _mm512_add_epi32(q5, _mm512_set1_epi32(j));
+    const __m512i lo = _mm512_permutex2var_epi32(v0, d, v1);
+    const __m512i mid = _mm512_permutex2var_epi32(v2, d, v3);
+    const __m512i hi = _mm512_permutexvar_epi32(d, v4);
+    const __mmask16 ge32 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(32));
+    const __mmask16 ge64 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(64));
+    const __m512i w = _mm512_mask_blend_epi32(ge64, _mm512_mask_blend_epi32(ge32, lo, mid), hi);
+    h = _mm512_mullo_epi32(_mm512_add_epi32(h, w), m);
+    h = _mm512_xor_si512(h, _mm512_srli_epi32(h, 16));
+  }
+  _mm512_storeu_si512(out, h);
+}
+bool has_avx512() {
+  static const bool has = __builtin_cpu_supports("avx512f");
+  return has;
+}
+#else
+bool has_avx512() { return false; }
+void hash20x16_avx512(const uint8_t*, uint32_t*) {}
+#endif
+
+uint32_t hash20(const uint8_t* p) {
+  uint32_t w[5];
+  std::memcpy(w, p, 20);  // little-endian host, like DecodeFixed32
+  uint32_t h = hash_init(20, kBloomSeed);
+  for (int j = 0; j < 5; j++) h = hash_word(h, w[j]);
+  return h;
+}
+
+// keys [lo, hi) of ks
+void hash_range(const dlsm_keyset& ks, uint64_t lo, uint64_t hi, uint32_t* out) {
+  const uint32_t sfx = ks.suffix_len;
+  if (!ks.offsets && ks.key_len == 20 + sfx) {
+    const uint64_t stride = ks.key_len;
+    uint64_t i = lo;
+    if (sfx == 0 && has_avx512())
+      for (; i + 16 <= hi; i += 16) hash20x16_avx512(ks.bytes + i * 20, out + i);
+    for (; i < hi; i++) out[i] = hash20(ks.bytes + i * stride);
+    return;
+  }
+  for (uint64_t i = lo; i < hi; i++) {
+    uint64_t s, l;
+    if (ks.offsets) {
+      s = ks.offsets[i];
+      l = ks.offsets[i + 1] - s;
+    } else {
+      s = i * ks.key_len;
+      l = ks.key_len;
+    }
+    l = l > sfx ? l - sfx : 0;  // ExtractUserKey (db/dbformat.h:374-377)
+    out[i] = bloom_hash_host(ks.bytes + s, l);
+  }
+}
+
+// Host cores this process may use: its CPU affinity set, capped by a cgroup
+// (v2) CPU quota when one is set -- on a shared GPU box the machine's CPU
+// count (hardware_concurrency) is many times the process's share.
+int usable_cores() {
+  int n = static_cast<int>(std::max(1u, std::thread::hardware_concurrency()));
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long long period = 0;
+    if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0 && period > 0) {
+      const long long quota = std::atoll(q);
+      if (quota > 0) n = std::min<int>(n, static_cast<int>(std::max(1LL, (quota + period - 1) / period)));
+    }
+    std::fclose(f);
+  }
+  return std::min(n, 64);
+}
+
+// A process-wide fork-join pool: run(parts, f) calls f(0..parts-1) on the
+// pool's threads and the caller, returning when all are done.  One run at a
+// time (callers serialise on run_m).
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool p;
+    return p;
+  }
+  int size() const { return static_cast<int>(th_.size()) + 1; }
+  void run(int parts, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> one(run_m_);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      f_ = &f;
+      parts_ = parts;
+      next_.store(0);
+      active_ = static_cast<int>(th_.size());
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return active_ == 0; });
+    f_ = nullptr;
+  }
+
+ private:
+  Pool() {
+    const int n = usable_cores() - 1;
+    for (int t = 0; t < n; t++) th_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      gen_++;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void work() {
+    for (int i; (i = next_.fetch_add(1)) < parts_;) (*f_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> lk(m_);
+      if (--active_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_, run_m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* f_ = nullptr;
+  std::atomic<int> next_{0};
+  int parts_ = 0, active_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+}  // namespace
+
+extern "C" int dlsm_bloom_hash_batch(const dlsm_keyset* keys, uint32_t* out, int threads) {
+  if (!keys || threads < 0) return DLSM_E_ARG;
+  const dlsm_keyset ks = *keys;
+  if (ks.n == 0) return DLSM_OK;
+  if (!out || !ks.bytes || ks.suffix_len > 255 || (!ks.offsets && ks.key_len < ks.suffix_len)) return DLSM_E_ARG;
+  constexpr uint64_t kPart = 1u << 16;  // keys per task (a multiple of 16)
+  const uint64_t parts = (ks.n + kPart - 1) / kPart;
+  Pool& pool = Pool::get();
+  const int width = threads == 0 ? pool.size() : std::min(threads, pool.size());
+  if (width <= 1 || parts == 1) {
+    hash_range(ks, 0, ks.n, out);
+    return DLSM_OK;
+  }
+  // `width` interleaved lanes of tasks: lane t takes parts t, t + width, ...
+  pool.run(width, [&](int t) {
+    for (uint64_t p = static_cast<uint64_t>(t); p < parts; p += static_cast<uint64_t>(width))
+      hash_range(ks, p * kPart, std::min(ks.n, (p + 1) * kPart), out);
+  });
+  return DLSM_OK;
+}

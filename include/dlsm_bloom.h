@@ -346,6 +346,21 @@ int dlsm_bloom_full_probe_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dls
 /* Host keys and host mask, synchronous. */
 int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
                           uint8_t* mask);
+/* The same probe from BloomHash values: `hashes` is a set of n u32 hashes
+ * (key_len 4, offsets NULL, suffix_len 0, 4-byte aligned, device memory) --
+ * what KeyMayMatch computes on the host (full_filter_block.cc:271) -- so a
+ * caller whose lookups start in host memory moves 4 bytes per key over PCIe
+ * instead of the key bytes (dlsm_bloom_hash_batch).  Asynchronous. */
+int dlsm_bloom_full_probe_hashed_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* hashes,
+                                     uint8_t* mask_dev);
+
+/* BloomHash (include/TimberSaw/filter_policy.h:26-28) of every key of a host
+ * key set (ExtractUserKey when suffix_len > 0) into out[n] (host), on up to
+ * `threads` host threads of a process-wide pool (0: all), sixteen 20-byte
+ * keys at a time with AVX-512 when the CPU has it.  The host side of the
+ * hashed build and probe: the hashes go to dlsm_bloom_full_build_hashed* /
+ * dlsm_bloom_full_probe_hashed_dev.  Synchronous; no device is touched. */
+int dlsm_bloom_hash_batch(const dlsm_keyset* keys, uint32_t* out, int threads);
 
 /* ---- MultiGet-style probe of a version's files ---- */
 

@@ -49,3 +49,38 @@ def test_step_roofline_and_pass_timing_note():
     assert abs(r["step_frac"] - r["step_alg_GBs"] / b.HBM_PEAK_GBS) < 1e-4
     assert "alone" in b.pass_timing_note(True, 12)["pass_timing"]
     assert "every 12-th" in b.pass_timing_note(False, 12)["pass_timing"]
+
+
+def test_threads_line_schema_per_gpu():
+    """The `--gpus N` line (one process, a thread per GPU) is self-describing:
+    every GPU's share with its own sampled pass times, rates and step time,
+    the imbalance between the slowest and fastest GPU, and the roofline of the
+    slowest GPU's dominant pass."""
+    import argparse
+    from types import SimpleNamespace
+
+    b = _bench()
+    n_gpu, T, N, Q, F, steps = 4, 16, 1_600_000, 100_000_000, 8, 20
+    args = argparse.Namespace(steps=steps, warmup=5, rehearse=False, path=0, probe_chunk_lg=13, probe_slice_lg=8)
+    workers, per_gpu = [], []
+    for r in range(n_gpu):
+        tables = list(range(r, T, n_gpu))
+        lo, hi = Q * r // n_gpu, Q * (r + 1) // n_gpu
+        workers.append(SimpleNamespace(work=SimpleNamespace(tables=tables, lookup_lo=lo, lookup_hi=hi), overlap=True))
+        passes = [(0.04 + 0.001 * r, 0.17 + 0.002 * r)] * 4
+        per_gpu.append(b.gpu_share_record(r, r, len(tables) * N, hi - lo, len(tables) * N * 21,
+                                          (hi - lo) * 21 + 16_000_552, passes, (0.2 + 0.01 * r) * steps / 1e3,
+                                          steps))
+    line = b.threads_line(args, n_gpu, list(range(n_gpu)), workers, per_gpu, 0.23 * steps / 1e3, T, N, Q, F, 10)
+    assert line["n_gpus"] == n_gpu and line["scaling"] == "strong"
+    assert abs(line["value"] - (T * N + Q) / 0.23e-3 / 1e6) < 1
+    assert [g["gpu"] for g in line["per_gpu"]] == list(range(n_gpu))
+    for g in line["per_gpu"]:
+        assert g["build_ms"] > 0 and g["probe_ms"] > 0 and g["ms_per_step"] > 0 and g["sampled_steps"] == 4
+        assert 0 < g["probe_frac"] < 1 and 0 < g["build_frac"] < 1
+    imb = line["imbalance"]
+    assert imb["slowest_gpu"] == n_gpu - 1 and imb["fastest_gpu"] == 0
+    assert abs(imb["max_over_min_ms_per_step"] - 0.23 / 0.2) < 1e-3
+    assert line["roofline"]["kernel"].startswith("probe pass of the slowest GPU")
+    assert line["roofline"]["frac"] == per_gpu[-1]["probe_frac"]
+    assert line["config"]["gpu_tables"][1] == list(range(1, T, n_gpu))

@@ -135,6 +135,12 @@ def test_bench_two_gpus_rehearsed():
     assert line["config"]["gpu_tables"] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
     assert line["config"]["gpu_lookups"] == [[0, 2_000_000], [2_000_000, 4_000_000]]
     assert line["value"] > 0 and line["roofline"]["achieved"] > 0
+    # self-describing: both GPUs' pass times, the imbalance, and the CPU baseline once
+    assert [g["gpu"] for g in line["per_gpu"]] == [0, 1]
+    assert all(g["build_ms"] > 0 and g["probe_ms"] > 0 and g["ms_per_step"] > 0 for g in line["per_gpu"])
+    assert line["imbalance"]["max_over_min_ms_per_step"] >= 1.0
+    cb = line["cpu_baseline"]
+    assert cb["cores"] >= 1 and cb["value"] > 0 and cb["gpu_output_matches_" + cb["kind"]]
 
 
 @pytest.mark.gpu
