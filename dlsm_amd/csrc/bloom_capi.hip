@@ -273,9 +273,15 @@ int choose_build_lgR(const std::vector<uint32_t>& Ls) {
     return ok;
   };
   uint64_t total = 0, t2 = 0;
+  // A/B knob: the slice-workgroup count below which the slices narrow
+  // (default two per CU)
+  static const uint64_t min_wgs = [] {
+    const char* e = getenv("DLSM_BUILD_SLICE_MIN_WGS");
+    return e ? strtoull(e, nullptr, 10) : 2ull * kBuildSliceCUs;
+  }();
   for (int lg = DLSM_BUILD_MIN_LGR; lg <= 11; lg++) {
     if (!slices(lg, &total)) continue;
-    while (lg > 7 && total < 2u * kBuildSliceCUs && slices(lg - 1, &t2)) {
+    while (lg > 7 && total < min_wgs && slices(lg - 1, &t2)) {
       lg--;
       total = t2;
     }

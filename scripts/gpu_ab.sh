@@ -12,7 +12,7 @@ for r in $(seq 1 "${ROUNDS:-3}"); do
     rest=${spec#*:}
     envs=${rest%%|*}
     args=${rest#*|}
-    env $envs timeout -k 10 180 python bench.py --steps 20 --warmup 5 --no-cpu --no-e2e $args \
+    env $envs timeout -k 10 180 python bench.py --steps 20 --warmup 5 --no-cpu --no-e2e --no-legacy $args \
       > "$OUT/${label}_$r.json" 2> "$OUT/${label}_$r.err" || exit 1
   done
 done

@@ -10,9 +10,10 @@
 #   smoke                       __graft_entry__.smoke()                   -> i_smoke.log
 #   bench [bench.py args]       one bench line                            -> i_bench.json
 #   kprof [bench.py args]       rocprofv3 --kernel-trace --stats of bench  -> i_prof/ + i_kernel_stats.txt
-#   pmc COUNTERS [bench args]   one rocprofv3 --pmc pass (quote counters as one word, comma-separated)
-#                                                                          -> i_pmc/
-#   ab ROUNDS SPEC...           interleaved A/B bench lines (SPEC = label:ENV=..|bench args) -> i_ab/
+#   pmc COUNTERS SCRIPT [args]  one rocprofv3 --pmc pass of python3 SCRIPT args (counters
+#                               comma-separated, one word)                 -> pmc/p<i>/
+#   ab ROUNDS SPECFILE          interleaved A/B bench lines, one spec "label:ENV=..|bench args"
+#                               per line of SPECFILE (scripts/ab/*.txt)   -> i_ab/
 #   builders THREADS MODES R    tests/cpp/concurrent_builders, THREADS/MODES comma lists, R rounds
 #                                                                          -> i_builders.jsonl
 #   run SECONDS CMD...          any other command under its own limit      -> i_run.log
@@ -42,18 +43,20 @@ for step in "$@"; do
         { echo "step $i failed" >> "$OUT/session.log"; exit 13; }
       python3 scripts/kstats.py "$OUT/${i}_prof" > "$OUT/${i}_kernel_stats.txt" 2>&1 || true ;;
     pmc)
-      read -r counters brest <<< "$rest"
-      timeout -s KILL 200 rocprofv3 --kernel-trace --pmc ${counters//,/ } --output-format csv -d "$OUT/${i}_pmc" -o run -- \
-        python3 bench.py $brest > "$OUT/${i}_pmc.json" 2> "$OUT/${i}_pmc.err" ||
+      # pmc COUNTERS SCRIPT [args]: one --pmc pass of `python3 SCRIPT args`
+      read -r counters script brest <<< "$rest"
+      timeout -s KILL 200 rocprofv3 --kernel-trace --pmc ${counters//,/ } --output-format csv -d "$OUT/pmc/p${i}" -o run -- \
+        python3 $script $brest > "$OUT/${i}_pmc.json" 2> "$OUT/${i}_pmc.err" ||
         { echo "step $i failed" >> "$OUT/session.log"; exit 14; } ;;
     ab)
-      read -r rounds specs <<< "$rest"
-      eval "set -- $specs"
-      ROUNDS=$rounds timeout -k 10 1000 bash scripts/gpu_ab.sh "$OUT/${i}_ab" "$@" ||
+      # ab ROUNDS SPECFILE: one "label:ENV=..|bench args" spec per line of SPECFILE
+      read -r rounds specfile <<< "$rest"
+      mapfile -t specs < "$specfile"
+      ROUNDS=$rounds timeout -k 10 1000 bash scripts/gpu_ab.sh "$OUT/${i}_ab" "${specs[@]}" ||
         { echo "step $i failed" >> "$OUT/session.log"; exit 15; } ;;
     builders)
       read -r threads modes rounds <<< "$rest"
-      [ -x "$OUT/cb" ] || g++ -std=c++17 -O2 -march=native -fno-rtti -fno-exceptions -pthread -I include \
+      [ -x "$OUT/cb" ] || g++ -std=c++17 -O2 -fno-rtti -fno-exceptions -pthread -I include \
         tests/cpp/concurrent_builders.cc -L dlsm_amd/lib -ldlsm_bloom -L oracle -loracle \
         -Wl,-rpath,$PWD/dlsm_amd/lib -Wl,-rpath,$PWD/oracle -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib \
         -o "$OUT/cb" || { echo "step $i: build failed" >> "$OUT/session.log"; exit 16; }
