@@ -110,10 +110,10 @@ struct LegacyTileJobDev {
 };
 constexpr uint32_t kLegacyTileLg = 16;  // bits per tile: 2^16 (8 KiB of LDS)
 #ifndef DLSM_LEGACY_CHUNK
-#define DLSM_LEGACY_CHUNK 2048  // keys per legacy partition chunk
+#define DLSM_LEGACY_CHUNK 4096  // keys per legacy partition chunk
 #endif
 #ifndef DLSM_LEGACY_NT
-#define DLSM_LEGACY_NT 256      // threads per legacy partition workgroup
+#define DLSM_LEGACY_NT 512      // threads per legacy partition workgroup
 #endif
 #ifndef DLSM_LEGACY_RANKED
 #define DLSM_LEGACY_RANKED 0    // 1: one ranked atomic pass (ranks kept in registers)

@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(kBlock) void probe_direct_kernel(const FilterDev* _
   const int mb = (F + 7) >> 3;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; i < kd.n;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    const uint32_t h = key_hash<MODE == KM_K20 ? KM_K20 : KM_GENERIC>(kd, i);
+    const uint32_t h = key_hash<(MODE == KM_K20 || MODE == KM_HASH) ? MODE : KM_GENERIC>(kd, i);
     for (int g = 0; g < mb; g++) {
       uint32_t m = 0;
       const int fe = min(F, 8 * g + 8);
