@@ -671,17 +671,25 @@ def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):
 
 
 def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_500_000, reps=3):
-    """Host-inclusive rate with the hashing on the host, as the reference does
-    it (BloomHash in AddKey and in KeyMayMatch, full_filter_block.cc:45,271):
-    keys start in pinned host memory, the host's cores hash them
-    (dlsm_bloom_hash_batch, inside the timed region), 4 B per key go H2D, the
-    GPU builds from the hashes (dlsm_bloom_full_build_hashed_dev) and probes
-    from them (dlsm_bloom_full_probe_hashed_dev), filters and masks come back
-    D2H into pinned memory.  The job is cut into chunks (the build's tables,
-    then lookup chunks) over two pinned hash buffers, so the host hashes chunk
-    i + 1 while chunk i's H2D copy and kernels run; the D2H copies run on a
-    second stream (PCIe is full duplex).  `ref` = (filters, mask) of the
-    device-resident run: the outputs are checked against them."""
+    """Host-inclusive rate with part of the hashing on the host, as the
+    reference does it (BloomHash in AddKey and in KeyMayMatch,
+    full_filter_block.cc:45,271).  Keys start in pinned host memory; filters
+    and masks end in pinned host memory.  Two feeds run at once:
+      - host-hashed lookups: the host's cores hash a chunk
+        (dlsm_bloom_hash_batch, inside the timed region), 4 B per key go H2D,
+        the GPU probes from the hashes (dlsm_bloom_full_probe_hashed_dev);
+        two pinned hash buffers, so the host hashes chunk i + 1 while chunk
+        i's copy and kernels run;
+      - raw keys: the build's tables and the first `raw` lookups go H2D as
+        20-byte keys on a second context and stream and are hashed on the GPU
+        (the DMA engines read them, not the host's cores).
+    Every key is read from host DRAM once either way (20 B); the split puts
+    as many keys on the host's cores as its DRAM read rate allows while the
+    PCIe link carries the rest: `raw` is chosen from the hash rate and the H2D
+    rate measured in the warm-up (time on the cores = time on the link).
+    D2H copies run on a third stream (PCIe is full duplex).  `ref` =
+    (filters, mask) of the device-resident run: the outputs are checked
+    against them."""
     import numpy as np
     import torch
 
@@ -691,60 +699,85 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     mb = fs.mask_bytes
     h_tabs = [t.data.cpu().pin_memory() for t in tables]
     h_q = qk.data.cpu().pin_memory()
-    cap = max(T * N, chunk_keys)
-    hb = [torch.empty(cap, dtype=torch.int32).pin_memory() for _ in range(2)]
+    q_np = h_q.numpy()
+    hb = [torch.empty(chunk_keys, dtype=torch.int32).pin_memory() for _ in range(2)]
     hb_np = [h.numpy() for h in hb]
-    db = [torch.empty(cap, dtype=torch.int32, device=dev) for _ in range(2)]
+    db = [torch.empty(chunk_keys, dtype=torch.int32, device=dev) for _ in range(2)]
+    d_tabs = [torch.empty_like(t.data) for t in tables]
+    d_q = torch.empty_like(qk.data)
     outs = [torch.zeros(dlsm_amd.full_size(t.n, bpk)[0] + 16, dtype=torch.uint8, device=dev) for t in tables]
     lens = torch.zeros(T, dtype=torch.uint64, device=dev)
     h_outs = [torch.empty_like(o, device="cpu").pin_memory() for o in outs]
     h_lens = torch.empty(T, dtype=torch.uint64).pin_memory()
     mask = torch.empty(Q * mb, dtype=torch.uint8, device=dev)
     h_mask = torch.empty(Q * mb, dtype=torch.uint8).pin_memory()
+    s_raw = torch.cuda.Stream(device=dev)
     s_out = torch.cuda.Stream(device=dev)
-    tab_np = [h.numpy() for h in h_tabs]
-    q_np = h_q.numpy()
-    chunks = [("build", 0, T * N)] + [("probe", lo, min(Q, lo + chunk_keys)) for lo in range(0, Q, chunk_keys)]
+    ctx_raw = dlsm_amd.Context(dev.index or 0)
+    ctx_raw.set_stream(s_raw)
 
-    def one_step():
+    def one_step(raw):
+        """raw: lookups [0, raw) go as keys, [raw, Q) hashed on the host."""
+        hash_s = 0.0
+        with torch.cuda.stream(s_raw):  # the raw feed, queued up front
+            for d, h in zip(d_tabs, h_tabs):
+                d.copy_(h, non_blocking=True)
+            if raw:
+                d_q[: raw * 20].copy_(h_q[: raw * 20], non_blocking=True)
+        ctx_raw.full_build_dev([dlsm_amd.Keys(d, t.n, 20) for d, t in zip(d_tabs, tables)], outs, lens, bpk)
+        if raw:
+            ctx_raw.full_probe_dev(fs, dlsm_amd.Keys(d_q[: raw * 20], raw, 20), mask[: raw * mb])
+        raw_done = torch.cuda.Event()
+        raw_done.record(s_raw)
+        s_out.wait_event(raw_done)
+        with torch.cuda.stream(s_out):
+            for h, o in zip(h_outs, outs):
+                h.copy_(o, non_blocking=True)
+            h_lens.copy_(lens, non_blocking=True)
+            h_mask[: raw * mb].copy_(mask[: raw * mb], non_blocking=True)
         free = [None, None]
-        for i, (kind, lo, hi) in enumerate(chunks):
-            b = i % 2
+        for i, lo in enumerate(range(raw, Q, chunk_keys)):
+            hi = min(Q, lo + chunk_keys)
+            n, b = hi - lo, i % 2
             if free[b] is not None:
                 free[b].synchronize()  # the H2D that last read this staging buffer
-            n = hi - lo
-            if kind == "build":
-                for s_, t in enumerate(tables):
-                    dlsm_amd.hash_batch(dlsm_amd.Keys(tab_np[s_], t.n, 20), out=hb_np[b][s_ * N:(s_ + 1) * N])
-            else:
-                dlsm_amd.hash_batch(dlsm_amd.Keys(q_np[lo * 20:hi * 20], n, 20), out=hb_np[b][:n])
+            t0 = time.perf_counter()
+            dlsm_amd.hash_batch(dlsm_amd.Keys(q_np[lo * 20:hi * 20], n, 20), out=hb_np[b][:n])
+            hash_s += time.perf_counter() - t0
             with torch.cuda.stream(stream):
                 db[b][:n].copy_(hb[b][:n], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
             free[b] = ev
-            if kind == "build":
-                ctx.full_build_hashed_dev([db[b][s_ * N:(s_ + 1) * N] for s_ in range(T)], outs, lens, bpk)
-            else:
-                ctx.full_probe_hashed_dev(fs, db[b][:n], mask[lo * mb:hi * mb], n)
+            ctx.full_probe_hashed_dev(fs, db[b][:n], mask[lo * mb:hi * mb], n)
             done = torch.cuda.Event()
             done.record(stream)
             s_out.wait_event(done)
             with torch.cuda.stream(s_out):
-                if kind == "build":
-                    for h, o in zip(h_outs, outs):
-                        h.copy_(o, non_blocking=True)
-                    h_lens.copy_(lens, non_blocking=True)
-                else:
-                    h_mask[lo * mb:hi * mb].copy_(mask[lo * mb:hi * mb], non_blocking=True)
+                h_mask[lo * mb:hi * mb].copy_(mask[lo * mb:hi * mb], non_blocking=True)
         stream.synchronize()
+        s_raw.synchronize()
         s_out.synchronize()
+        return hash_s
 
-    one_step()  # warm-up (workspaces, pool threads)
+    # warm-up: workspaces, pool threads, and the two rates the split is set by
+    hashed_keys = Q - chunk_keys
+    hs = one_step(chunk_keys)
+    hash_rate = hashed_keys / hs  # keys/s on the host's cores
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(s_raw):
+        d_q.copy_(h_q, non_blocking=True)
+    s_raw.synchronize()
+    h2d_Bps = h_q.numel() / (time.perf_counter() - t0)
+    # raw lookups r: (Q - r) / hash_rate = (20 (T N + r) + 4 (Q - r)) / h2d_Bps
+    r = (Q / hash_rate - (20 * T * N + 4 * Q) / h2d_Bps) / (1 / hash_rate + 16 / h2d_Bps)
+    raw = int(min(Q, max(0, round(r / 4096) * 4096)))
+    one_step(raw)
     times = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        one_step()
+        one_step(raw)
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times))
     L = h_lens.numpy()
@@ -752,13 +785,17 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     ok = (all(h_outs[s_][: int(L[s_])].numpy().tobytes() == ref_filters[s_] for s_ in range(T))
           and bool(np.array_equal(h_mask.numpy(), ref_mask)))
     nk = T * N + Q
+    ctx_raw.close()
     return {"mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
             "ms_per_step_reps": [round(x * 1e3, 3) for x in times],
+            "host_hashed_keys": Q - raw, "raw_keys": T * N + raw,
+            "host_hash_gkeys_s": round(hash_rate / 1e9, 3), "h2d_GBs": round(h2d_Bps / 1e9, 1),
             "host_hash_threads": "all usable cores (dlsm_bloom_hash_batch pool)",
-            "chunk_keys": chunk_keys, "h2d_bytes_per_key": 4,
+            "chunk_keys": chunk_keys, "h2d_bytes_per_key": {"host_hashed": 4, "raw": 20},
             "matches_device_resident": ok,
-            "note": ("host BloomHash (timed) + H2D 4 B/key hashes + hashed build / probe + D2H filters/masks, "
-                     "chunked, pinned host buffers")}
+            "note": ("host BloomHash (timed) of the lookups the host's DRAM rate allows, 4 B/key H2D, hashed probe; "
+                     "the build's tables and the other lookups H2D as 20-byte keys on a second stream, hashed on "
+                     "the GPU; D2H filters/masks on a third stream; pinned host buffers")}
 
 
 def host_cores() -> int:

@@ -2,6 +2,7 @@
 // device workspace, job set-up, and the host-buffer (staged) call variants.
 // Kernels live in bloom_kernels.hip.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <atomic>
@@ -174,6 +175,13 @@ struct dlsm_ctx {
   hipEvent_t up_ev[kUpSlots] = {};
   bool up_live[kUpSlots] = {};
   int up_next = 0;
+  // How a host-API call waits for its stream (ctx_sync): 0 hipStreamSynchronize,
+  // 1 poll an event, yielding the core between polls, 2 a blocking-sync event
+  // (DLSM_HOST_SYNC; default 1).  Many builder threads (dLSM runs 28) share
+  // the host's cores with the HIP runtime's own threads: a waiter that spins
+  // holds a core the other builders' AddKey hashing needs.
+  int host_sync = 1;
+  hipEvent_t ev_wait = nullptr;      // ctx_sync modes 1 and 2
 };
 
 // A stacked image of the filters of one mask byte that share a line count
@@ -208,6 +216,16 @@ struct dlsm_filterset {
 };
 
 namespace {
+
+// Wait until everything queued on s so far has completed (see host_sync).
+hipError_t ctx_sync(dlsm_ctx* ctx, hipStream_t s) {
+  if (ctx->host_sync == 0 || !ctx->ev_wait) return hipStreamSynchronize(s);
+  hipError_t e = hipEventRecord(ctx->ev_wait, s);
+  if (e != hipSuccess) return e;
+  if (ctx->host_sync == 2) return hipEventSynchronize(ctx->ev_wait);
+  while ((e = hipEventQuery(ctx->ev_wait)) == hipErrorNotReady) sched_yield();
+  return e;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -506,6 +524,10 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
     ctx->up_cap[i] = dlsm_ctx::kUpSlotBytes;
     e = hipEventCreateWithFlags(&ctx->up_ev[i], hipEventDisableTiming);
   }
+  if (const char* v = getenv("DLSM_HOST_SYNC")) ctx->host_sync = atoi(v);
+  if (e == hipSuccess)
+    e = hipEventCreateWithFlags(&ctx->ev_wait, hipEventDisableTiming |
+                                                   (ctx->host_sync == 2 ? hipEventBlockingSync : 0u));
   ctx->stream = ctx->own;
   if (e != hipSuccess) {
     dlsm_ctx_destroy(ctx);
@@ -552,6 +574,7 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->crc_cap.release();
   ctx->crc_val.release();
   if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_wait) (void)hipEventDestroy(ctx->ev_wait);
   if (ctx->ev_pfork) (void)hipEventDestroy(ctx->ev_pfork);
   if (ctx->ev_pdone) (void)hipEventDestroy(ctx->ev_pdone);
   for (int b = 0; b < kStageEvents; b++) {
@@ -610,7 +633,7 @@ int dlsm_stream_destroy(void* s) {
 int dlsm_ctx_sync(dlsm_ctx* ctx) {
   if (!ctx) return DLSM_E_ARG;
   DeviceGuard g(ctx->device);
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  DLSM_TRY(ctx_sync(ctx, ctx->stream));
   return DLSM_OK;
 }
 
@@ -1126,7 +1149,7 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
     for (int j = 0; j < n_jobs; j++) dj[j].out = ctx->st_out.p + opos[j];
     DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p, hashed));
     DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
-    DLSM_TRY(hipStreamSynchronize(s));
+    DLSM_TRY(ctx_sync(ctx, s));
     int st = DLSM_OK;
     for (int j = 0; j < n_jobs; j++) {
       if (out_len[j] == 0) {
@@ -1135,7 +1158,7 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
       }
       DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
     }
-    DLSM_TRY(hipStreamSynchronize(s));
+    DLSM_TRY(ctx_sync(ctx, s));
     return st;
   }
   DLSM_CHECK(host_ensure(ctx->h_out, ctx->h_out_cap, obytes + 256));
@@ -1145,7 +1168,7 @@ int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, 
   if (!h_out_dev || !h_len_dev) return DLSM_E_DEVICE;
   for (int j = 0; j < n_jobs; j++) dj[j].out = direct[j] ? direct[j] : h_out_dev + opos[j];
   DLSM_CHECK(full_build_dev_impl(ctx, dj.data(), n_jobs, bits_per_key, h_len_dev, hashed));
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   int st = DLSM_OK;
   for (int j = 0; j < n_jobs; j++) {
     out_len[j] = ctx->h_len[j];
@@ -1277,7 +1300,7 @@ int dlsm_bloom_full_build_block(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
   DLSM_CHECK(dlsm_bloom_full_build_block_dev(ctx, dj.data(), n_jobs, bits_per_key, ctx->st_len.p));
   hipStream_t s = ctx->stream;
   DLSM_TRY(hipMemcpyAsync(out_len, ctx->st_len.p, sizeof(uint64_t) * n_jobs, hipMemcpyDeviceToHost, s));
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   int st = DLSM_OK;
   for (int j = 0; j < n_jobs; j++) {
     if (out_len[j] == 0) {
@@ -1286,7 +1309,7 @@ int dlsm_bloom_full_build_block(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
     }
     DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
   }
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   return st;
 }
 
@@ -1305,7 +1328,7 @@ int dlsm_crc32c_dev(dlsm_ctx* ctx, const uint8_t* const* bufs, const uint64_t* l
   DLSM_CHECK(ctx->crc_val.ensure(n));
   DLSM_CHECK(run_crc(ctx, st, n, max_total, nullptr, nullptr, nullptr, ctx->crc_val.p));
   DLSM_TRY(hipMemcpyAsync(crc_out, ctx->crc_val.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  DLSM_TRY(ctx_sync(ctx, ctx->stream));
   return DLSM_OK;
 }
 
@@ -1335,7 +1358,7 @@ int dlsm_internal_keys_select_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, int p
     DLSM_TRY(launch_key_select(to_desc(k), policy, smallest_snapshot, keep_dev, bc, bb,
                                reinterpret_cast<unsigned long long*>(bad), tot, s));
     DLSM_TRY(hipMemcpyAsync(res, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-    DLSM_TRY(hipStreamSynchronize(s));
+    DLSM_TRY(ctx_sync(ctx, s));
   }
   if (n_kept) *n_kept = res[0];
   if (kept_bytes) *kept_bytes = res[1];
@@ -1386,7 +1409,7 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
     const uint8_t* tp = filters[f] + lens[f] - 5;
     if (filters_are_device) {
       DLSM_TRY(hipMemcpyAsync(tail, tp, 5, hipMemcpyDeviceToHost, s));
-      DLSM_TRY(hipStreamSynchronize(s));
+      DLSM_TRY(ctx_sync(ctx, s));
     } else {
       memcpy(tail, tp, 5);
     }
@@ -1725,7 +1748,7 @@ int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_ke
   DLSM_CHECK(ctx->st_out.ensure(mb));
   DLSM_CHECK(dlsm_bloom_full_probe_dev(ctx, fs, &dk[0], ctx->st_out.p));
   DLSM_TRY(hipMemcpyAsync(mask, ctx->st_out.p, mb, hipMemcpyDeviceToHost, ctx->stream));
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  DLSM_TRY(ctx_sync(ctx, ctx->stream));
   return DLSM_OK;
 }
 
@@ -1818,7 +1841,7 @@ int dlsm_filter_block_build_dev(dlsm_ctx* ctx, const dlsm_keyset* keys, const ui
   tail.back() = static_cast<uint8_t>(kFilterBaseLg);
   DLSM_TRY(hipMemcpyAsync(out_dev + G.array_offset, tail.data(), tail.size(), hipMemcpyHostToDevice,
                           ctx->stream));
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));  // `tail` is pageable host memory
+  DLSM_TRY(ctx_sync(ctx, ctx->stream));  // `tail` is pageable host memory
   if (out_len) *out_len = G.total;
   return DLSM_OK;
 }
@@ -1853,7 +1876,7 @@ int dlsm_filter_block_build(dlsm_ctx* ctx, const dlsm_keyset* keys, const uint64
   DLSM_CHECK(dlsm_filter_block_build_dev(ctx, &dk[0], block_key_end, block_end_offset, n_blocks,
                                          bits_per_key, ctx->st_out.p, need, &len));
   DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p, len, hipMemcpyDeviceToHost, ctx->stream));
-  DLSM_TRY(hipStreamSynchronize(ctx->stream));
+  DLSM_TRY(ctx_sync(ctx, ctx->stream));
   if (out_len) *out_len = len;
   return DLSM_OK;
 }
@@ -1879,7 +1902,7 @@ int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, c
                                          reinterpret_cast<const uint64_t*>(ctx->st_out.p + bo),
                                          ctx->st_out.p + oo));
   DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p + oo, keys->n, hipMemcpyDeviceToHost, s));
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   return DLSM_OK;
 }
 
@@ -1965,7 +1988,7 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
     uint8_t tail[5];
     if (filters_are_device) {
       DLSM_TRY(hipMemcpyAsync(tail, F.filter + F.filter_len - 5, 5, hipMemcpyDeviceToHost, s));
-      DLSM_TRY(hipStreamSynchronize(s));
+      DLSM_TRY(ctx_sync(ctx, s));
     } else {
       memcpy(tail, F.filter + F.filter_len - 5, 5);
     }
@@ -2214,7 +2237,7 @@ int dlsm_bloom_legacy_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_job
     out_len[j] = dj[j].out_cap;
     DLSM_TRY(hipMemcpyAsync(jobs[j].out, dj[j].out, out_len[j], hipMemcpyDeviceToHost, s));
   }
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   return DLSM_OK;
 }
 
@@ -2234,7 +2257,7 @@ int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64
   } else {
     uint8_t kb;
     DLSM_TRY(hipMemcpyAsync(&kb, filter_dev + len - 1, 1, hipMemcpyDeviceToHost, s));
-    DLSM_TRY(hipStreamSynchronize(s));
+    DLSM_TRY(ctx_sync(ctx, s));
     const int ks = static_cast<int>(static_cast<int8_t>(kb));
     if (ks < 0 || ks > 30) trivial = 2;
     else if (ks == 0) trivial = 2;  // zero probes -> match
@@ -2267,7 +2290,7 @@ int dlsm_bloom_legacy_probe(dlsm_ctx* ctx, const uint8_t* filter, uint64_t len,
   DLSM_CHECK(ctx->st_out.ensure(keys->n));
   DLSM_CHECK(dlsm_bloom_legacy_probe_dev(ctx, fdev, len, &dk[0], ctx->st_out.p));
   DLSM_TRY(hipMemcpyAsync(out, ctx->st_out.p, keys->n, hipMemcpyDeviceToHost, s));
-  DLSM_TRY(hipStreamSynchronize(s));
+  DLSM_TRY(ctx_sync(ctx, s));
   return DLSM_OK;
 }
 

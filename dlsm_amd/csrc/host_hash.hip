@@ -8,7 +8,7 @@
 // (memtable / compaction iterators, Get() callers) can hash them here and
 // hand the GPU 4 bytes per key (dlsm_bloom_full_build_hashed*,
 // dlsm_bloom_full_probe_hashed_dev) instead of the key bytes: a quarter of
-// the PCIe traffic for 20-byte keys.  Sixteen 20-byte keys at a time with
+// the PCIe traffic for 20-byte keys.  Thirty-two 20-byte keys at a time with
 // AVX-512 when the CPU has it, on a process-wide pool of host threads.
 #include <hip/hip_runtime.h>  // bloom_math.h's host/device qualifiers
 
@@ -40,29 +40,57 @@ using dlsm::hash_word;
 using dlsm::kBloomSeed;
 using dlsm::kHashM;
 
-// Sixteen 20-byte keys at p .. p + 300 (util/hash.cc's five rounds on all
-// sixteen at once): the 80 dwords load as five vectors, dword j of key q
-// (5q + j) is gathered across them with two-source permutes.
 #if defined(__x86_64__)
-__attribute__((target("avx512f"))) void hash20x16_avx512(const uint8_t* p, uint32_t* out) {
-  const __m512i v0 = _mm512_loadu_si512(p), v1 = _mm512_loadu_si512(p + 64), v2 = _mm512_loadu_si512(p + 128),
-                v3 = _mm512_loadu_si512(p + 192), v4 = _mm512_loadu_si512(p + 256);
+// One 16-key group's gather indices and masks, per round j (constants).
+struct Group16 {
+  __m512i d[5];
+  __mmask16 ge32[5], ge64[5];
+};
+__attribute__((target("avx512f"))) inline Group16 group16() {
+  Group16 g;
   const __m512i q5 = _mm512_mullo_epi32(_mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15),
                                         _mm512_set1_epi32(5));
-  const __m512i m = _mm512_set1_epi32(static_cast<int>(kHashM));
-  __m512i h = _mm512_set1_epi32(static_cast<int>(hash_init(20, kBloomSeed)));
   for (int j = 0; j < 5; j++) {
-    const __m512i d = _mm512_add_epi32(q5, _mm512_set1_epi32(j));
-    const __m512i lo = _mm512_permutex2var_epi32(v0, d, v1);
-    const __m512i mid = _mm512_permutex2var_epi32(v2, d, v3);
-    const __m512i hi = _mm512_permutexvar_epi32(d, v4);
-    const __mmask16 ge32 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(32));
-    const __mmask16 ge64 = _mm512_cmpge_epu32_mask(d, _mm512_set1_epi32(64));
-    const __m512i w = _mm512_mask_blend_epi32(ge64, _mm512_mask_blend_epi32(ge32, lo, mid), hi);
-    h = _mm512_mullo_epi32(_mm512_add_epi32(h, w), m);
-    h = _mm512_xor_si512(h, _mm512_srli_epi32(h, 16));
+    g.d[j] = _mm512_add_epi32(q5, _mm512_set1_epi32(j));
+    g.ge32[j] = _mm512_cmpge_epu32_mask(g.d[j], _mm512_set1_epi32(32));
+    g.ge64[j] = _mm512_cmpge_epu32_mask(g.d[j], _mm512_set1_epi32(64));
   }
-  _mm512_storeu_si512(out, h);
+  return g;
+}
+// Dword j of the sixteen 20-byte keys held in v0..v4 (key q's dword j is
+// dword 5q + j of the 320 bytes): two-source permutes + blends.
+__attribute__((target("avx512f"))) inline __m512i word16(const Group16& g, int j, __m512i v0, __m512i v1,
+                                                         __m512i v2, __m512i v3, __m512i v4) {
+  const __m512i lo = _mm512_permutex2var_epi32(v0, g.d[j], v1);
+  const __m512i mid = _mm512_permutex2var_epi32(v2, g.d[j], v3);
+  const __m512i hi = _mm512_permutexvar_epi32(g.d[j], v4);
+  return _mm512_mask_blend_epi32(g.ge64[j], _mm512_mask_blend_epi32(g.ge32[j], lo, mid), hi);
+}
+// Keys [0, n) of the fixed 20-byte batch at p (n a multiple of 32): util/hash.cc's
+// five rounds on two groups of sixteen keys at once -- two independent
+// multiply chains per iteration (the round's multiply latency is the
+// critical path) -- with the key stream prefetched 2 KiB ahead.
+__attribute__((target("avx512f"))) void hash20_avx512(const uint8_t* p, uint64_t n, uint32_t* out) {
+  const Group16 g = group16();
+  const __m512i m = _mm512_set1_epi32(static_cast<int>(kHashM));
+  const __m512i h0 = _mm512_set1_epi32(static_cast<int>(hash_init(20, kBloomSeed)));
+  for (uint64_t i = 0; i < n; i += 32, p += 640, out += 32) {
+    for (int c = 0; c < 640; c += 64) _mm_prefetch(reinterpret_cast<const char*>(p + 2048 + c), _MM_HINT_T0);
+    const __m512i a0 = _mm512_loadu_si512(p), a1 = _mm512_loadu_si512(p + 64), a2 = _mm512_loadu_si512(p + 128),
+                  a3 = _mm512_loadu_si512(p + 192), a4 = _mm512_loadu_si512(p + 256);
+    const __m512i b0 = _mm512_loadu_si512(p + 320), b1 = _mm512_loadu_si512(p + 384),
+                  b2 = _mm512_loadu_si512(p + 448), b3 = _mm512_loadu_si512(p + 512),
+                  b4 = _mm512_loadu_si512(p + 576);
+    __m512i ha = h0, hb = h0;
+    for (int j = 0; j < 5; j++) {
+      ha = _mm512_mullo_epi32(_mm512_add_epi32(ha, word16(g, j, a0, a1, a2, a3, a4)), m);
+      hb = _mm512_mullo_epi32(_mm512_add_epi32(hb, word16(g, j, b0, b1, b2, b3, b4)), m);
+      ha = _mm512_xor_si512(ha, _mm512_srli_epi32(ha, 16));
+      hb = _mm512_xor_si512(hb, _mm512_srli_epi32(hb, 16));
+    }
+    _mm512_storeu_si512(out, ha);
+    _mm512_storeu_si512(out + 16, hb);
+  }
 }
 bool has_avx512() {
   static const bool has = __builtin_cpu_supports("avx512f");
@@ -70,7 +98,7 @@ bool has_avx512() {
 }
 #else
 bool has_avx512() { return false; }
-void hash20x16_avx512(const uint8_t*, uint32_t*) {}
+void hash20_avx512(const uint8_t*, uint64_t, uint32_t*) {}
 #endif
 
 uint32_t hash20(const uint8_t* p) {
@@ -87,8 +115,11 @@ void hash_range(const dlsm_keyset& ks, uint64_t lo, uint64_t hi, uint32_t* out) 
   if (!ks.offsets && ks.key_len == 20 + sfx) {
     const uint64_t stride = ks.key_len;
     uint64_t i = lo;
-    if (sfx == 0 && has_avx512())
-      for (; i + 16 <= hi; i += 16) hash20x16_avx512(ks.bytes + i * 20, out + i);
+    if (sfx == 0 && has_avx512() && hi - lo >= 32) {
+      const uint64_t n32 = (hi - lo) & ~uint64_t(31);
+      hash20_avx512(ks.bytes + lo * 20, n32, out + lo);
+      i = lo + n32;
+    }
     for (; i < hi; i++) out[i] = hash20(ks.bytes + i * stride);
     return;
   }
@@ -200,7 +231,7 @@ extern "C" int dlsm_bloom_hash_batch(const dlsm_keyset* keys, uint32_t* out, int
   const dlsm_keyset ks = *keys;
   if (ks.n == 0) return DLSM_OK;
   if (!out || !ks.bytes || ks.suffix_len > 255 || (!ks.offsets && ks.key_len < ks.suffix_len)) return DLSM_E_ARG;
-  constexpr uint64_t kPart = 1u << 16;  // keys per task (a multiple of 16)
+  constexpr uint64_t kPart = 1u << 14;  // keys per task (a multiple of 32)
   const uint64_t parts = (ks.n + kPart - 1) / kPart;
   Pool& pool = Pool::get();
   const int width = threads == 0 ? pool.size() : std::min(threads, pool.size());

@@ -211,6 +211,15 @@ int main(int argc, char** argv) {
     ge = std::max(ge, r.gpu_end);
     ce = std::max(ce, r.cpu_end);
   }
+  // Finish calls over 2 ms, by the thread's table index (1 = its first timed table)
+  std::string slow = "[";
+  for (int q = 0; q < tables; q++) {
+    int c = 0;
+    for (auto& r : res) c += q < static_cast<int>(r.finish_ms.size()) && r.finish_ms[q] > 2.0;
+    slow += (q ? ", " : "") + std::to_string(c);
+  }
+  slow += "]";
+  const char* hs = std::getenv("DLSM_HOST_SYNC");
   std::sort(lat.begin(), lat.end());
   const auto pct = [&](double p) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, static_cast<size_t>(p * lat.size()))]; };
   double sum = 0;
@@ -222,12 +231,13 @@ int main(int argc, char** argv) {
       "{\"mode\": \"%s\", \"batches\": %llu, \"mean_batch\": %.2f, \"max_batch\": %llu, "
       "\"threads\": %d, \"tables_per_thread\": %d, \"keys_per_table\": %d, \"failures\": %d, "
       "\"no_device_alloc_after_warmup\": %s, \"finish_ms\": {\"median\": %.4f, \"p90\": %.4f, \"p99\": %.4f, "
-      "\"max\": %.4f, \"mean\": %.4f}, \"addkey_ns_per_key\": %.2f, "
+      "\"max\": %.4f, \"mean\": %.4f}, \"finish_over_2ms_by_table\": %s, \"host_sync\": \"%s\", "
+      "\"addkey_ns_per_key\": %.2f, "
       "\"gpu_adapter\": {\"wall_ms\": %.2f, \"mkeys_s\": %.1f, \"tables_per_s\": %.0f}, "
       "\"cpu_oracle_same_threads\": {\"wall_ms\": %.2f, \"mkeys_s\": %.1f, \"ms_per_table\": %.3f}}\n",
       mode.c_str(), static_cast<unsigned long long>(nb), nb ? static_cast<double>(nj) / nb : 0.0,
       static_cast<unsigned long long>(mb), threads, tables, n, fails, no_alloc ? "true" : "false", pct(0.5), pct(0.9), pct(0.99),
-      lat.empty() ? 0.0 : lat.back(), lat.empty() ? 0.0 : sum / lat.size(),
+      lat.empty() ? 0.0 : lat.back(), lat.empty() ? 0.0 : sum / lat.size(), slow.c_str(), hs ? hs : "default",
       add_ms * 1e6 / keys_timed, gpu_ms, keys_timed / (gpu_ms * 1e3), threads * tables / (gpu_ms * 1e-3),
       cpu_ms, keys_timed / (cpu_ms * 1e3), cpu_ms * threads / (threads * tables));
   if (fails == 0 && no_alloc) std::printf("OK concurrent builders\n");

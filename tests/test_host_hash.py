@@ -9,7 +9,7 @@ import dlsm_amd
 
 
 def test_hash_batch_fixed20_vs_oracle(orc):
-    for n in (1, 15, 16, 17, 65_535, 65_536, 65_537, 300_001):
+    for n in (1, 15, 16, 17, 31, 32, 33, 63, 64, 65, 65_535, 65_536, 65_537, 300_001):
         k = orc.dbbench_keys(7, 13, n)
         got = dlsm_amd.hash_batch(dlsm_amd.Keys(k, n, 20))
         idx = np.unique(np.concatenate([np.arange(min(n, 64)), np.arange(0, n, 997), [n - 1]]))
