@@ -678,8 +678,8 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
       - host-hashed lookups: the host's cores hash a chunk
         (dlsm_bloom_hash_batch, inside the timed region), 4 B per key go H2D,
         the GPU probes from the hashes (dlsm_bloom_full_probe_hashed_dev);
-        two pinned hash buffers, so the host hashes chunk i + 1 while chunk
-        i's copy and kernels run;
+        the host hashes chunk i + 1 while chunk i's copy and kernels run
+        (a pinned hash slot per lookup: no staging to wait for);
       - raw keys: the build's tables and the first `raw` lookups go H2D as
         20-byte keys on a second context and stream and are hashed on the GPU
         (the DMA engines read them, not the host's cores).
@@ -700,9 +700,11 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     h_tabs = [t.data.cpu().pin_memory() for t in tables]
     h_q = qk.data.cpu().pin_memory()
     q_np = h_q.numpy()
-    hb = [torch.empty(chunk_keys, dtype=torch.int32).pin_memory() for _ in range(2)]
-    hb_np = [h.numpy() for h in hb]
-    db = [torch.empty(chunk_keys, dtype=torch.int32, device=dev) for _ in range(2)]
+    # one pinned slot per lookup's hash: the host never waits for a copy to
+    # free its staging (the raw feed's copies hold the link for most of the step)
+    hb = torch.empty(Q, dtype=torch.int32).pin_memory()
+    hb_np = hb.numpy()
+    db = torch.empty(Q, dtype=torch.int32, device=dev)
     d_tabs = [torch.empty_like(t.data) for t in tables]
     d_q = torch.empty_like(qk.data)
     outs = [torch.zeros(dlsm_amd.full_size(t.n, bpk)[0] + 16, dtype=torch.uint8, device=dev) for t in tables]
@@ -735,21 +737,15 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
                 h.copy_(o, non_blocking=True)
             h_lens.copy_(lens, non_blocking=True)
             h_mask[: raw * mb].copy_(mask[: raw * mb], non_blocking=True)
-        free = [None, None]
-        for i, lo in enumerate(range(raw, Q, chunk_keys)):
+        for lo in range(raw, Q, chunk_keys):
             hi = min(Q, lo + chunk_keys)
-            n, b = hi - lo, i % 2
-            if free[b] is not None:
-                free[b].synchronize()  # the H2D that last read this staging buffer
+            n = hi - lo
             t0 = time.perf_counter()
-            dlsm_amd.hash_batch(dlsm_amd.Keys(q_np[lo * 20:hi * 20], n, 20), out=hb_np[b][:n])
+            dlsm_amd.hash_batch(dlsm_amd.Keys(q_np[lo * 20:hi * 20], n, 20), out=hb_np[lo:hi])
             hash_s += time.perf_counter() - t0
             with torch.cuda.stream(stream):
-                db[b][:n].copy_(hb[b][:n], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            free[b] = ev
-            ctx.full_probe_hashed_dev(fs, db[b][:n], mask[lo * mb:hi * mb], n)
+                db[lo:hi].copy_(hb[lo:hi], non_blocking=True)
+            ctx.full_probe_hashed_dev(fs, db[lo:hi], mask[lo * mb:hi * mb], n)
             done = torch.cuda.Event()
             done.record(stream)
             s_out.wait_event(done)

@@ -1566,12 +1566,18 @@ uint32_t group_slices(const dlsm_ctx* ctx, const ProbeGroup& g, int* lgR, uint32
 // (slice, part) workgroups of the slice pass: about one resident wave of
 // workgroups (256 CUs x 2 slices of 64 KiB or 1 of 128 KiB), each part at
 // least one chunk per wave (a part's waves split its chunks into equal
-// groups).  ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU.)
+// groups).  ($DLSM_SLICE_WGS_PER_CU overrides the 2 / 1 slices per CU,
+// $DLSM_SLICE_PARTS the parts: A/B knobs.)
 int slice_parts(uint32_t S, uint32_t nC, int lgR) {
   static const uint32_t per_cu_env = [] {
     const char* e = getenv("DLSM_SLICE_WGS_PER_CU");
     return e ? static_cast<uint32_t>(atoi(e)) : 0u;
   }();
+  static const int parts_env = [] {  // A/B knob: parts per slice
+    const char* e = getenv("DLSM_SLICE_PARTS");
+    return e ? atoi(e) : 0;
+  }();
+  if (parts_env > 0) return parts_env;
   const uint32_t resident = 256u * (per_cu_env ? per_cu_env : (lgR == 7 ? 2u : 1u));
   int parts = static_cast<int>(std::max<uint32_t>(1, (resident + S / 2) / S));
   return std::min<int>(parts, static_cast<int>(std::max<uint32_t>(1, nC / 16)));

@@ -19,7 +19,8 @@ import sys
 from collections import defaultdict
 
 PASSES = {"probe": ("probe_partition_kernel", "probe_slice_kernel", "probe_unpermute_kernel"),
-          "build": ("full_partition_kernel", "full_slice_kernel")}
+          "build": ("full_partition_kernel", "full_slice_kernel"),
+          "legacy": ("legacy_partition_kernel", "legacy_slice_kernel")}
 
 
 def per_kernel(pmc_dir):
@@ -36,9 +37,9 @@ def main():
     pmc_dir, bench_json, out_json = sys.argv[1:4]
     bench = json.load(open(bench_json))
     vals = per_kernel(pmc_dir)
-    out = {"source": pmc_dir, "config": {k: bench["config"][k] for k in
+    out = {"source": pmc_dir, "config": {k: bench.get("config", bench).get(k) for k in
                                           ("tables", "keys_per_table", "lookups", "filters",
-                                           "probe_chunk_lg", "probe_slice_lg")},
+                                           "probe_chunk_lg", "probe_slice_lg", "keys")},
            "note": "per launch of the pass; FETCH_SIZE x2 (gfx950), KiB -> bytes; "
                    "fabric traffic incl. Infinity-Cache hits"}
     for name, kernels in PASSES.items():
@@ -53,6 +54,8 @@ def main():
             detail[k] = {"fetch_bytes": round(fb), "write_bytes": round(wb)}
             fetch += fb
             write += wb
+        if not detail:
+            continue
         out[name] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
                      "traffic_bytes": round(fetch + write), "kernels": detail}
     json.dump(out, open(out_json, "w"), indent=1)
