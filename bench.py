@@ -420,6 +420,11 @@ def main():
     legacy_out = None
     if world == 1 and tables and not args.no_legacy:
         result["legacy"], legacy_out = legacy_leg(ctx, stream, tables, bpk)
+        lt = load_traffic(args.traffic, result["config"], "legacy") if world == 1 else None
+        if lt:  # PMC fabric bytes of one legacy batch build (partition + slice)
+            result["legacy"]["traffic"] = lt["traffic_bytes"]
+            result["legacy"]["traffic_alg_ratio"] = round(
+                lt["traffic_bytes"] / (result["legacy"]["alg_bytes_per_key"] * len(tables) * tables[0].n), 3)
 
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if world == 1 and rank == 0 and not args.no_cpu:

@@ -115,9 +115,6 @@ constexpr uint32_t kLegacyTileLg = 16;  // bits per tile: 2^16 (8 KiB of LDS)
 #ifndef DLSM_LEGACY_NT
 #define DLSM_LEGACY_NT 512      // threads per legacy partition workgroup
 #endif
-#ifndef DLSM_LEGACY_RANKED
-#define DLSM_LEGACY_RANKED 0    // 1: one ranked atomic pass (ranks kept in registers)
-#endif
 constexpr int kLegacyChunk = DLSM_LEGACY_CHUNK;
 constexpr int kLegacyPartBlock = DLSM_LEGACY_NT;
 // Partition variants (static LDS staging of one chunk region of u16 entries:

@@ -1777,27 +1777,6 @@ __global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
   const int k = J.k;
   for (uint32_t b = tid; b <= nT; b += NT) hist[b] = 0;
   __syncthreads();
-#if DLSM_LEGACY_RANKED
-  // one ranked pass: each position's rank inside its tile bucket (u16, two
-  // per register); the scatter recomputes the position and reads its
-  // bucket's start
-  uint32_t rk[(PER * KMAX + 1) / 2];
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
-    uint32_t hh = h[r];
-    const uint32_t delta = bloom_delta(hh);
-#pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-      const int x = r * KMAX + q;
-      if (live && q < k) {
-        const uint32_t rank = atomicAdd(&hist[fastmod(hh, bits, magic) >> kLegacyTileLg], 1u);
-        rk[x >> 1] = (x & 1) ? (rk[x >> 1] | (rank << 16)) : rank;
-      }
-      hh += delta;
-    }
-  }
-#else
   // Count the positions per tile (the positions are computed twice -- here
   // and in the scatter -- rather than kept: 8 keys x k codes per thread would
   // hold ~50 more VGPRs and halve the workgroups per CU).
@@ -1812,7 +1791,6 @@ __global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
       hh += delta;
     }
   }
-#endif
   __syncthreads();
   for (uint32_t b = tid; b < nT; b += NT) {  // pad every bucket to whole 16-byte units
     const uint32_t cnt = hist[b];
@@ -1825,33 +1803,6 @@ __global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
   uint16_t* trow = tab + J.tab0 + static_cast<uint64_t>(c) * (nT + 1);
   for (uint32_t b = tid; b <= nT; b += NT) trow[b] = static_cast<uint16_t>(hist[b]);
   uint16_t* stage = reinterpret_cast<uint16_t*>(tile);  // free since hash_chunk's last barrier
-#if DLSM_LEGACY_RANKED
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
-    uint32_t hh = h[r];
-    const uint32_t delta = bloom_delta(hh);
-#pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-      const int x = r * KMAX + q;
-      if (live && q < k) {
-        const uint32_t bp = fastmod(hh, bits, magic);
-        const uint32_t rank = (x & 1) ? (rk[x >> 1] >> 16) : (rk[x >> 1] & 0xffffu);
-        stage[hist[bp >> kLegacyTileLg] + rank] = static_cast<uint16_t>(bp);
-      }
-      hh += delta;
-    }
-  }
-  __syncthreads();
-  for (uint32_t b = tid; b < nT; b += NT) {  // pads: copies of the bucket's last position
-    const uint32_t np = npad[b];
-    if (np) {
-      const uint32_t end = hist[b + 1] - np;
-      const uint16_t v = stage[end - 1];
-      for (uint32_t p = 0; p < np; p++) stage[end + p] = v;
-    }
-  }
-#else
   __syncthreads();  // hist becomes the buckets' fill cursors
   // Scatter: a bucket's order is whatever the LDS atomics give -- the slice
   // pass ORs bits, so the order of a tile's positions never shows.
@@ -1878,7 +1829,6 @@ __global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
       for (uint32_t p = 0; p < np; p++) stage[end + p] = v;
     }
   }
-#endif
   __syncthreads();
   store_chunk_u16<NT>(entries + J.entry0 + static_cast<uint64_t>(c) * J.region, stage, total);
 }

@@ -22,7 +22,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   mkdir -p "$OUT/pmc" &&
   timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-legacy $BARGS > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $BARGS > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
 done &&
 python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" > /dev/null &&
 timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
