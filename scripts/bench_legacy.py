@@ -48,7 +48,8 @@ def main():
     want = oracle.legacy_build(keys[0].data.cpu().numpy(), N, bpk=a.bpk)
     ok = outs[0][: int(L[0])].cpu().numpy().tobytes() == want
     alg = T * N * 20 + int(L.sum())
-    print(json.dumps({"variant": os.environ.get("DLSM_LIB_VARIANT", "base"), "tables": T, "keys": N,
+    print(json.dumps({"variant": os.environ.get("DLSM_LIB_VARIANT", "base"),
+                      "env": {k: v for k, v in os.environ.items() if k.startswith("DLSM_LEGACY")}, "tables": T, "keys": N,
                       "ms": round(ms, 4), "mkeys_s": round(T * N / ms / 1e3, 1),
                       "alg_GBs": round(alg / ms / 1e6, 1), "frac": round(alg / ms / 1e6 / 8000, 4),
                       "table0_matches_oracle": ok}))
