@@ -228,6 +228,7 @@ def main():
             elapsed, passes = MG.native_run([dwork], args.steps, 0, bpk)
         else:
             elapsed, passes = MG.native_run([dwork], args.steps, args.warmup, bpk)
+        own_elapsed = elapsed
         elapsed = SH.max_over_ranks(elapsed, dist, dev)
         build_ms = float(np.mean([b for b, _ in passes]))
         probe_ms = float(np.mean([p for _, p in passes]))
@@ -302,6 +303,7 @@ def main():
         if dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        own_elapsed = elapsed
         elapsed = SH.max_over_ranks(elapsed, dist, dev)
     if not use_native and (cosched or not pass_events):
         # co-scheduled passes overlap, so the per-pass times (roofline) come
@@ -427,6 +429,13 @@ def main():
                 lt["traffic_bytes"] / (result["legacy"]["alg_bytes_per_key"] * len(tables) * tables[0].n), 3)
 
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
+    if dist:  # every rank's share, so the N-GPU line shows each GPU's passes
+        mine = gpu_share_record(rank, local, len(tables) * N, qk.n, build_bytes, probe_bytes,
+                                [(build_ms, probe_ms)], own_elapsed, args.steps)
+        recs = [None] * world
+        dist.all_gather_object(recs, mine)
+        result["per_gpu"] = recs
+        result["imbalance"] = imbalance(recs)
     if world == 1 and rank == 0 and not args.no_cpu:
         filters = [f for f in inp.filters]
         L = lens.cpu().numpy()
@@ -532,7 +541,6 @@ def threads_line(args, n_gpu, devices, workers, per_gpu, elapsed, T, N, Q, F, bp
     slowest GPU's share."""
     value = (T * N + Q) * args.steps / elapsed / 1e6
     slow = max(per_gpu, key=lambda r: r["ms_per_step"])
-    fast = min(per_gpu, key=lambda r: r["ms_per_step"])
     dominant = "probe" if (slow["probe_ms"] or 0) >= (slow["build_ms"] or 0) else "build"
     ach = slow[dominant + "_alg_GBs"] or 0.0
     step_bytes = sum(r["build_keys"] * 21.25 + r["probe_keys"] * 21.16 for r in per_gpu)
@@ -575,13 +583,20 @@ def threads_line(args, n_gpu, devices, workers, per_gpu, elapsed, T, N, Q, F, bp
             **step_roofline(step_bytes, elapsed / args.steps),
         },
         "per_gpu": per_gpu,
-        "imbalance": {"slowest_gpu": slow["gpu"], "fastest_gpu": fast["gpu"],
-                      "max_over_min_ms_per_step": round(slow["ms_per_step"] / fast["ms_per_step"], 4)
-                      if fast["ms_per_step"] > 0 else None,
-                      "max_minus_min_ms_per_step": round(slow["ms_per_step"] - fast["ms_per_step"], 4)},
+        "imbalance": imbalance(per_gpu),
         "build": {"ms": slow["build_ms"], "note": "slowest GPU's share; per_gpu has every GPU"},
         "probe": {"ms": slow["probe_ms"], "note": "slowest GPU's share; per_gpu has every GPU"},
     }
+
+
+def imbalance(per_gpu):
+    """Slowest vs fastest GPU of an N-GPU line (by each GPU's own step time)."""
+    slow = max(per_gpu, key=lambda r: r["ms_per_step"])
+    fast = min(per_gpu, key=lambda r: r["ms_per_step"])
+    return {"slowest_gpu": slow["gpu"], "fastest_gpu": fast["gpu"],
+            "max_over_min_ms_per_step": round(slow["ms_per_step"] / fast["ms_per_step"], 4)
+            if fast["ms_per_step"] > 0 else None,
+            "max_minus_min_ms_per_step": round(slow["ms_per_step"] - fast["ms_per_step"], 4)}
 
 
 def event_stride_of(steps):

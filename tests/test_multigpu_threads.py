@@ -187,3 +187,7 @@ def test_bench_under_launcher_two_ranks_rehearsed():
     assert line["config"]["rank0_tables"] == list(range(0, 16, 2))
     assert line["config"]["rank0_lookups"] == 2_000_000
     assert line["value"] > 0 and line["probe"]["ms"] > 0 and line["build"]["ms"] > 0
+    # every rank's share, gathered to rank 0
+    assert [r["gpu"] for r in line["per_gpu"]] == [0, 1]
+    assert all(r["build_ms"] > 0 and r["probe_ms"] > 0 and r["probe_keys"] == 2_000_000 for r in line["per_gpu"])
+    assert line["imbalance"]["max_over_min_ms_per_step"] >= 1.0
