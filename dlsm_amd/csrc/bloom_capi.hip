@@ -4,8 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <sched.h>
 
-#include <cmath>
-
 #include <algorithm>
 #include <atomic>
 #include <map>
@@ -2129,25 +2127,6 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
     fits_b = fits_b && ok && nt <= kLegacyTilesB && reg <= kLegacyStageB;
   }
   const int mode = all_k20 ? KM_K20 : (all_k28 ? KM_K28 : KM_GENERIC);
-  // Variant NC (no count pass): a fixed bucket per tile of cap entries, cap =
-  // the chunk's expected positions per tile + sigma standard deviations + 8
-  // (Poisson), rounded up to whole 16-byte units.  $DLSM_LEGACY_NC=0 keeps
-  // the counted partition; $DLSM_LEGACY_NC_SIGMA sets sigma (default 2.6;
-  // tests lower it to drive the spill and fallback paths).
-  std::vector<int32_t> caps(n_jobs, 0);
-  bool nc = k <= kLegacyKmaxA && fits_a;
-  {
-    const char* e = getenv("DLSM_LEGACY_NC");
-    if (e && atoi(e) == 0) nc = false;
-  }
-  double sigma = 2.6;
-  if (const char* e = getenv("DLSM_LEGACY_NC_SIGMA")) sigma = atof(e);
-  for (int j = 0; j < n_jobs && nc; j++) {
-    const double mu = static_cast<double>(k) * kLegacyChunk / std::max<uint32_t>(1, tiles[j]);
-    const uint64_t cap = (static_cast<uint64_t>(std::ceil(mu + sigma * std::sqrt(mu))) + 8 + 7) & ~uint64_t(7);
-    caps[j] = static_cast<int32_t>(std::min<uint64_t>(cap, kLegacyStageNC));
-    nc = tiles[j] <= kLegacyTilesNC && static_cast<uint64_t>(tiles[j]) * cap <= kLegacyStageNC;
-  }
   if (ctx->path != 1 && fits_b) {
     const int tps_lg = choose_legacy_tps_lg(tiles);
     std::vector<LegacyTileJobDev> hj(n_jobs);
@@ -2171,7 +2150,7 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
       d.n_slices = (tiles[j] + (1u << tps_lg) - 1) >> tps_lg;
       d.slice0 = slice;
       d.k = k;
-      d.reserved = nc ? caps[j] : 0;
+      d.reserved = 0;
       starts[j] = chunk;
       starts[n_jobs + j] = slice;
       entry += static_cast<uint64_t>(d.n_chunks) * d.region;
@@ -2186,7 +2165,7 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
     DLSM_CHECK(ctx_upload(ctx, ctx->ltjobs.p, hj.data(), sizeof(LegacyTileJobDev) * n_jobs, s));
     DLSM_CHECK(ctx_upload(ctx, ctx->ltstarts.p, starts.data(), sizeof(uint32_t) * 2 * n_jobs, s));
     DLSM_TRY(launch_legacy_partition(ctx->ltjobs.p, ctx->ltstarts.p, n_jobs, chunk, ctx->lentries.p, ctx->ltab.p,
-                                     nc ? 2 : (fits_a ? 0 : 1), mode, s));
+                                     fits_a ? 0 : 1, mode, s));
     DLSM_TRY(launch_legacy_slices(ctx->ltjobs.p, ctx->ltstarts.p + n_jobs, n_jobs, slice, ctx->lentries.p,
                                   ctx->ltab.p, tps_lg, s));
     return DLSM_OK;

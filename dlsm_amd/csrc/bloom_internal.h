@@ -106,7 +106,7 @@ struct LegacyTileJobDev {
   uint32_t chunk0, n_chunks;
   uint32_t slice0, n_slices;
   int32_t k;
-  int32_t reserved;    // variant NC: bucket capacity per tile (a multiple of 8)
+  int32_t reserved;
 };
 constexpr uint32_t kLegacyTileLg = 16;  // bits per tile: 2^16 (8 KiB of LDS)
 #ifndef DLSM_LEGACY_CHUNK
@@ -129,11 +129,6 @@ constexpr uint32_t legacy_region(int k, uint32_t tiles) {
 }
 constexpr uint32_t kLegacyStageA = legacy_region(kLegacyKmaxA, kLegacyTilesA);
 constexpr uint32_t kLegacyStageB = legacy_region(kLegacyKmaxB, kLegacyTilesB);
-// Variant NC (legacy_partition_nc_kernel, no count pass): k <= 6, <= 255
-// tiles, tiles x cap staged u16 entries (cap: LegacyTileJobDev::reserved).
-constexpr uint32_t kLegacyStageNC = 35840;  // staged u16 entries (70 KiB)
-constexpr uint32_t kLegacyTilesNC = 255;    // bucket ids fit a byte (0xff: "tail unit")
-constexpr uint32_t kLegacySpillNC = 512;    // spilled positions per chunk before the counted fallback
 constexpr int kLegacySliceBlock = 1024;
 
 constexpr int kBlock = 256;
@@ -226,7 +221,7 @@ hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s
                                  uint64_t total_keys, int mode, hipStream_t s);
 hipError_t launch_legacy_probe(const uint8_t* filter, uint64_t bits, uint32_t magic, int k,
                                int trivial, KeyDesc keys, uint8_t* out, int mode, hipStream_t s);
-// LDS-tiled legacy build: variant 0 = A, 1 = B, 2 = NC (kLegacy*); tps_lg 0..4 tiles
+// LDS-tiled legacy build: variant 0 = A, 1 = B (kLegacy*); tps_lg 0..4 tiles
 // per slice workgroup (log2).
 hipError_t launch_legacy_partition(const LegacyTileJobDev* jobs, const uint32_t* chunk0s, int n_jobs,
                                    uint32_t total_chunks, uint16_t* entries, uint16_t* tab, int variant,

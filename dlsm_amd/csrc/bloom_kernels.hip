@@ -1745,16 +1745,34 @@ __global__ __launch_bounds__(kBlock) void legacy_probe_kernel(const uint8_t* __r
 // kernel's 6 device-scope atomicOr per key are memory-side operations on
 // 64 random rows per wave instruction.
 // ---------------------------------------------------------------------------
-// The counted partition of one chunk whose keys' hashes are in h (the key
-// tile is free): count per tile, pad, scan, table row, scatter, store.
-// stage holds the chunk's region (>= J.region entries), hist nT + 1 bins.
-template <int KMAX, int PER>
-__device__ __forceinline__ void legacy_counted(const LegacyTileJobDev& J, uint32_t c, uint32_t nk,
-                                               const uint32_t (&h)[PER], uint16_t* stage, uint32_t* hist,
-                                               uint8_t* npad, uint32_t* wsum, uint16_t* __restrict__ entries,
-                                               uint16_t* __restrict__ tab) {
+template <int MODE, int KMAX, uint32_t STAGE, uint32_t TMAX>
+__global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
+    const LegacyTileJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
+    uint16_t* __restrict__ entries, uint16_t* __restrict__ tab) {
   constexpr int NT = kLegacyPartBlock;
+  constexpr int C = kLegacyChunk;
+  constexpr int PER = C / NT;
+  constexpr int KB = mode_kb<MODE>();
+  constexpr int TKV = K20Tile<NT, tile_kpt<KB>(), KB>::kVec;  // uint4 of one key tile
+  constexpr int SV = static_cast<int>(STAGE / 8u);            // uint4 of one staged region
+  constexpr int TVB = TKV > SV ? TKV : SV;
+  static_assert(TMAX + 1 <= 4u * NT, "block_excl_scan_lds covers the tile bins");
+  __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
+  __shared__ uint32_t hist[TMAX + 1];
+  __shared__ uint8_t npad[TMAX];
+  __shared__ uint32_t wsum[NT / 64];
+  __shared__ int sj;
   const int tid = threadIdx.x;
+  const uint32_t bid = blockIdx.x;
+  if (tid == 0) sj = find_job(chunk0s, n_jobs, bid);
+  __syncthreads();
+  const LegacyTileJobDev J = jobs[sj];
+  const uint32_t c = bid - J.chunk0;
+  const uint64_t first = static_cast<uint64_t>(c) * C;
+  const uint64_t left = J.keys.n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
+  uint32_t h[PER];
+  hash_chunk<MODE, NT, PER>(J.keys, first, nk, tile, h);
   const uint32_t nT = J.n_tiles, bits = J.bits, magic = J.magic;
   const int k = J.k;
   for (uint32_t b = tid; b <= nT; b += NT) hist[b] = 0;
@@ -1784,6 +1802,7 @@ __device__ __forceinline__ void legacy_counted(const LegacyTileJobDev& J, uint32
   const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(nT + 1), wsum);
   uint16_t* trow = tab + J.tab0 + static_cast<uint64_t>(c) * (nT + 1);
   for (uint32_t b = tid; b <= nT; b += NT) trow[b] = static_cast<uint16_t>(hist[b]);
+  uint16_t* stage = reinterpret_cast<uint16_t*>(tile);  // free since hash_chunk's last barrier
   __syncthreads();  // hist becomes the buckets' fill cursors
   // Scatter: a bucket's order is whatever the LDS atomics give -- the slice
   // pass ORs bits, so the order of a tile's positions never shows.
@@ -1812,166 +1831,6 @@ __device__ __forceinline__ void legacy_counted(const LegacyTileJobDev& J, uint32
   }
   __syncthreads();
   store_chunk_u16<NT>(entries + J.entry0 + static_cast<uint64_t>(c) * J.region, stage, total);
-}
-
-template <int MODE, int KMAX, uint32_t STAGE, uint32_t TMAX>
-__global__ __launch_bounds__(kLegacyPartBlock) void legacy_partition_kernel(
-    const LegacyTileJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
-    uint16_t* __restrict__ entries, uint16_t* __restrict__ tab) {
-  constexpr int NT = kLegacyPartBlock;
-  constexpr int C = kLegacyChunk;
-  constexpr int PER = C / NT;
-  constexpr int KB = mode_kb<MODE>();
-  constexpr int TKV = K20Tile<NT, tile_kpt<KB>(), KB>::kVec;  // uint4 of one key tile
-  constexpr int SV = static_cast<int>(STAGE / 8u);            // uint4 of one staged region
-  constexpr int TVB = TKV > SV ? TKV : SV;
-  static_assert(TMAX + 1 <= 4u * NT, "block_excl_scan_lds covers the tile bins");
-  __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
-  __shared__ uint32_t hist[TMAX + 1];
-  __shared__ uint8_t npad[TMAX];
-  __shared__ uint32_t wsum[NT / 64];
-  __shared__ int sj;
-  const int tid = threadIdx.x;
-  const uint32_t bid = blockIdx.x;
-  if (tid == 0) sj = find_job(chunk0s, n_jobs, bid);
-  __syncthreads();
-  const LegacyTileJobDev J = jobs[sj];
-  const uint32_t c = bid - J.chunk0;
-  const uint64_t first = static_cast<uint64_t>(c) * C;
-  const uint64_t left = J.keys.n - first;
-  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
-  uint32_t h[PER];
-  hash_chunk<MODE, NT, PER>(J.keys, first, nk, tile, h);  // ends with a barrier: the tile is free
-  legacy_counted<KMAX, PER>(J, c, nk, h, reinterpret_cast<uint16_t*>(tile), hist, npad, wsum, entries, tab);
-}
-
-// The partition without the count pass (variant NC: k <= 6, <= 255 tiles):
-// every tile gets a fixed-capacity bucket of J.reserved (= cap, a multiple of
-// 8) entries in LDS, sized from the chunk's expected count per tile (k C /
-// tiles + 2.6 standard deviations + 8), so ONE pass of LDS atomics places
-// every position.  A position past its bucket's capacity goes to a spill
-// list (tile << 16 | position).  Then the buckets' counts (their cursors)
-// are padded and scanned into the table row as before, a unit -> bucket map
-// routes each 16-byte output unit to its bucket's staged unit, and the rare
-// overfull bucket's tail (its spilled positions, then its pads) is written
-// by its own thread.  A chunk whose spills overflow the list (never at these
-// capacities; forced by tests) falls back to the counted partition.
-template <int MODE>
-__global__ __launch_bounds__(kLegacyPartBlock, 4) void legacy_partition_nc_kernel(
-    const LegacyTileJobDev* __restrict__ jobs, const uint32_t* __restrict__ chunk0s, int n_jobs,
-    uint16_t* __restrict__ entries, uint16_t* __restrict__ tab) {
-  constexpr int NT = kLegacyPartBlock;
-  constexpr int C = kLegacyChunk;
-  constexpr int PER = C / NT;
-  constexpr int KMAX = kLegacyKmaxA;
-  constexpr int KB = mode_kb<MODE>();
-  constexpr int TKV = K20Tile<NT, tile_kpt<KB>(), KB>::kVec;
-  constexpr int SV = static_cast<int>(kLegacyStageNC / 8u);
-  constexpr int TVB = TKV > SV ? TKV : SV;
-  static_assert(kLegacyStageNC >= legacy_region(KMAX, kLegacyTilesNC), "the counted fallback fits the stage");
-  __shared__ __attribute__((aligned(16))) uint4 tile[TVB];
-  __shared__ uint32_t hist[kLegacyTilesNC + 1];
-  __shared__ uint8_t npad[kLegacyTilesNC];
-  __shared__ uint8_t umap[kLegacyStageNC / 8];
-  __shared__ uint32_t spill[kLegacySpillNC];
-  __shared__ uint32_t wsum[NT / 64];
-  __shared__ uint32_t nsp;
-  __shared__ int sj;
-  const int tid = threadIdx.x;
-  const uint32_t bid = blockIdx.x;
-  if (tid == 0) sj = find_job(chunk0s, n_jobs, bid);
-  __syncthreads();
-  const LegacyTileJobDev J = jobs[sj];
-  const uint32_t c = bid - J.chunk0;
-  const uint64_t first = static_cast<uint64_t>(c) * C;
-  const uint64_t left = J.keys.n - first;
-  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : C;
-  uint32_t h[PER];
-  hash_chunk<MODE, NT, PER>(J.keys, first, nk, tile, h);  // ends with a barrier: the tile is free
-  uint16_t* stage = reinterpret_cast<uint16_t*>(tile);
-  const uint32_t nT = J.n_tiles, bits = J.bits, magic = J.magic;
-  const uint32_t cap = static_cast<uint32_t>(J.reserved);
-  const int k = J.k;
-  for (uint32_t b = tid; b < nT; b += NT) hist[b] = b * cap;  // bucket cursors
-  if (tid == 0) nsp = 0;
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < PER; r++) {
-    const bool live = static_cast<uint32_t>(r * NT + tid) < nk;
-    uint32_t hh = h[r];
-    const uint32_t delta = bloom_delta(hh);
-#pragma unroll
-    for (int q = 0; q < KMAX; q++) {
-      if (live && q < k) {
-        const uint32_t bp = fastmod(hh, bits, magic);
-        const uint32_t t = bp >> kLegacyTileLg;
-        const uint32_t slot = atomicAdd(&hist[t], 1u);
-        if (slot < (t + 1u) * cap) {
-          stage[slot] = static_cast<uint16_t>(bp);
-        } else {
-          const uint32_t x = atomicAdd(&nsp, 1u);
-          if (x < kLegacySpillNC) spill[x] = (t << 16) | (bp & 0xffffu);
-        }
-      }
-      hh += delta;
-    }
-  }
-  __syncthreads();
-  const uint32_t n_spill = nsp;  // block-uniform
-  if (n_spill > kLegacySpillNC) {  // the spill list overflowed: count, as the other variant
-    // (the chunk is hashed again rather than h kept live through the scatter)
-    uint32_t h2[PER];
-    hash_chunk<MODE, NT, PER>(J.keys, first, nk, tile, h2);
-    legacy_counted<KMAX, PER>(J, c, nk, h2, stage, hist, npad, wsum, entries, tab);
-    return;
-  }
-  for (uint32_t b = tid; b <= nT; b += NT) {  // counts (padded to whole units) for the scan
-    if (b == nT) {
-      hist[b] = 0;
-      continue;
-    }
-    const uint32_t cnt = hist[b] - b * cap;
-    const uint32_t pad = (0u - cnt) & 7u;
-    npad[b] = static_cast<uint8_t>(pad);
-    hist[b] = cnt + pad;
-  }
-  __syncthreads();
-  const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(nT + 1), wsum);
-  uint16_t* trow = tab + J.tab0 + static_cast<uint64_t>(c) * (nT + 1);
-  for (uint32_t b = tid; b <= nT; b += NT) trow[b] = static_cast<uint16_t>(hist[b]);
-  uint16_t* out = entries + J.entry0 + static_cast<uint64_t>(c) * J.region;
-  for (uint32_t b = tid; b < nT; b += NT) {
-    const uint32_t np = npad[b];
-    const uint32_t cnt = hist[b + 1] - hist[b] - np;
-    const uint32_t u0 = hist[b] / 8u, nu = (cnt + np) / 8u;
-    const uint32_t staged = min(nu, cap / 8u);  // units staged in the bucket (whole, pads included)
-    for (uint32_t u = 0; u < staged; u++) umap[u0 + u] = static_cast<uint8_t>(b);
-    for (uint32_t u = staged; u < nu; u++) umap[u0 + u] = 0xffu;
-    if (cnt <= cap) {  // pads: copies of the bucket's last position
-      if (np) {
-        const uint16_t v = stage[b * cap + cnt - 1u];
-        for (uint32_t p = 0; p < np; p++) stage[b * cap + cnt + p] = v;
-      }
-    } else {  // overfull: the tail past the staged units -- spilled positions, then pads
-      uint32_t o = hist[b] + cap;
-      uint16_t v = 0;
-      for (uint32_t x = 0; x < n_spill; x++) {
-        const uint32_t e = spill[x];
-        if ((e >> 16) == b) {
-          v = static_cast<uint16_t>(e);
-          out[o++] = v;
-        }
-      }
-      for (uint32_t p = 0; p < np; p++) out[o++] = v;
-    }
-  }
-  __syncthreads();
-  const uint4* st4 = reinterpret_cast<const uint4*>(stage);
-  uint4* o4 = reinterpret_cast<uint4*>(out);
-  for (uint32_t u = tid; u < total / 8u; u += NT) {
-    const uint32_t b = umap[u];
-    if (b != 0xffu) o4[u] = st4[(b * cap + u * 8u - hist[b]) / 8u];
-  }
 }
 
 // One chunk's run of a legacy slice, as one wave sees it: lane j <= tn holds
@@ -2665,16 +2524,6 @@ hipError_t launch_legacy_partition(const LegacyTileJobDev* jobs, const uint32_t*
                                    uint32_t total_chunks, uint16_t* entries, uint16_t* tab, int variant,
                                    int mode, hipStream_t s) {
   if (total_chunks == 0) return hipSuccess;
-  if (variant == 2) {
-    if (mode == KM_K20)
-      legacy_partition_nc_kernel<KM_K20><<<total_chunks, kLegacyPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, entries, tab);
-    else if (mode == KM_K28)
-      legacy_partition_nc_kernel<KM_K28><<<total_chunks, kLegacyPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, entries, tab);
-    else
-      legacy_partition_nc_kernel<KM_GENERIC><<<total_chunks, kLegacyPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, entries,
-                                                                                       tab);
-    return hipGetLastError();
-  }
 #define DLSM_LPART(MM, KM, ST, TM) \
   legacy_partition_kernel<MM, KM, ST, TM><<<total_chunks, kLegacyPartBlock, 0, s>>>(jobs, chunk0s, n_jobs, entries, tab)
 #define DLSM_LPART_V(MM)                                                   \

@@ -210,32 +210,3 @@ def test_back_to_back_batches_without_sync(gpu, orc):
             nf, nl = int(lf.cpu()[s]), int(ll.cpu()[s])
             assert of[s][:nf].cpu().numpy().tobytes() == want_f[r][s], (r, s)
             assert ol[s][:nl].cpu().numpy().tobytes() == want_l[r][s], (r, s)
-
-
-@pytest.mark.parametrize("sigma,nc", [("2.6", "1"), ("1.0", "1"), ("0", "1"), ("-3", "1"), ("2.6", "0")])
-def test_legacy_partition_variants(gpu, orc, sigma, nc, monkeypatch):
-    """The partition without a count pass (variant NC: fixed buckets per tile,
-    a spill list, a counted fallback per chunk) against the counted one:
-    bucket capacity sigma = 2.6 (default: spills are rare), 1.0 and 0
-    (spills in most chunks), -3 (the spill list overflows: every chunk falls
-    back to the counted partition), and NC off.  Tables of 1.6 M keys (245 tiles), 153,846 keys (24 tiles)
-    and a ragged 70,001-key table in one batch, every byte vs the oracle."""
-    import torch
-
-    import dlsm_amd
-
-    monkeypatch.setenv("DLSM_LEGACY_NC_SIGMA", sigma)
-    monkeypatch.setenv("DLSM_LEGACY_NC", nc)
-    sizes = [1_600_000, 153_846, 70_001]
-    tabs = [orc.dbbench_keys(s + 40, 3, n) for s, n in enumerate(sizes)]
-    keys = [dlsm_amd.Keys(torch.from_numpy(t).cuda(), n, 20) for t, n in zip(tabs, sizes)]
-    outs = [torch.full((dlsm_amd.legacy_size(n) + 64,), 0xEE, dtype=torch.uint8, device="cuda") for n in sizes]
-    lens = torch.zeros(3, dtype=torch.uint64, device="cuda")
-    gpu.legacy_build_dev(keys, outs, lens, 10)
-    gpu.sync()
-    L = lens.cpu().numpy()
-    for s, (t, n) in enumerate(zip(tabs, sizes)):
-        want = orc.legacy_build(t, n)
-        assert int(L[s]) == len(want), (s, sigma)
-        assert outs[s][: int(L[s])].cpu().numpy().tobytes() == want, (s, sigma, nc)
-        assert (outs[s][int(L[s]):].cpu().numpy() == 0xEE).all(), (s, sigma)
