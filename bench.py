@@ -777,9 +777,9 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
         return hash_s
 
     # warm-up: workspaces, pool threads, and the two rates the split is set by
-    hashed_keys = Q - chunk_keys
-    hs = one_step(chunk_keys)
-    hash_rate = hashed_keys / hs  # keys/s on the host's cores
+    raw0 = min(chunk_keys, Q // 2)
+    hs = one_step(raw0)
+    hash_rate = (Q - raw0) / max(hs, 1e-9)  # keys/s on the host's cores
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(s_raw):
