@@ -210,3 +210,34 @@ def test_back_to_back_batches_without_sync(gpu, orc):
             nf, nl = int(lf.cpu()[s]), int(ll.cpu()[s])
             assert of[s][:nf].cpu().numpy().tobytes() == want_f[r][s], (r, s)
             assert ol[s][:nl].cpu().numpy().tobytes() == want_l[r][s], (r, s)
+
+
+def test_legacy_probe_at_config2_size(gpu, orc):
+    """util/bloom.cc KeyMayMatch (util/bloom.cc:57-81) against a 1.6 M-key
+    legacy filter built on the GPU: 4 M lookups (the table's own keys, then
+    random db_bench keys) through the device probe, every answer vs the
+    oracle; members always match, the others at ~1 % (10 bits/key)."""
+    import torch
+
+    import dlsm_amd
+
+    n, q = 1_600_000, 4_000_000
+    t = orc.dbbench_keys(3, 16, n)
+    keys = [dlsm_amd.Keys(torch.from_numpy(t).cuda(), n, 20)]
+    out = torch.zeros(dlsm_amd.legacy_size(n) + 16, dtype=torch.uint8, device="cuda")
+    lens = torch.zeros(1, dtype=torch.uint64, device="cuda")
+    gpu.legacy_build_dev(keys, [out], lens, 10)
+    gpu.sync()
+    L = int(lens.cpu()[0])
+    filt = out[:L].cpu().numpy().tobytes()
+    assert filt == orc.legacy_build(t, n)
+    look = np.concatenate([t[: 20 * (q // 2)].reshape(-1),
+                           orc.keys_from_values(orc.mt_values(77, 1 << 40, q - q // 2)).reshape(-1)])
+    ans = torch.zeros(q, dtype=torch.uint8, device="cuda")
+    gpu.legacy_probe_dev(out, L, dlsm_amd.Keys(torch.from_numpy(look).cuda(), q, 20), ans)
+    gpu.sync()
+    got = ans.cpu().numpy()
+    want = orc.legacy_probe(filt, look, q)
+    assert np.array_equal(got, want)
+    assert got[: q // 2].all()
+    assert 0.005 < got[q // 2:].mean() < 0.02
