@@ -2210,11 +2210,16 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, u
                                      uint16_t* tab, int mode, hipStream_t s, uint32_t cus) {
   const uint32_t nC = static_cast<uint32_t>((keys.n + C - 1) / C);
   if (nC == 0) return hipSuccess;
-  // persistent: a few resident workgroups per CU loop over the chunks
-  // ($DLSM_PART_GRID_PER_CU, default 2; 0 = one workgroup per chunk)
+  // One workgroup per chunk (default), or persistent: $DLSM_PART_GRID_PER_CU
+  // resident workgroups per CU looping over the chunks with the next chunk's
+  // key tiles in flight.  Round 4 (`profiles/r04_o_grid0_shares_ab.txt`): one
+  // workgroup per chunk takes the probe pass 0.685 -> 0.645 ms and the
+  // overlapped step -4 % (the hardware's dispatcher keeps every CU's phases
+  // mixed, with no tail of long-running workgroups and room for the build's
+  // workgroups beside them); neutral at the N = 4 / 8 shares.
   static const uint32_t per_cu = [] {
     const char* e = getenv("DLSM_PART_GRID_PER_CU");
-    return e ? static_cast<uint32_t>(atoi(e)) : 2u;
+    return e ? static_cast<uint32_t>(atoi(e)) : 0u;
   }();
   const uint32_t g = per_cu ? std::min(nC, per_cu * (cus ? cus : device_cus())) : nC;
   // $DLSM_PROBE_PLAIN_STORES=1: plain (Infinity-Cache-allocating) intermediate
