@@ -1194,7 +1194,10 @@ __device__ __forceinline__ void for_buckets(uint32_t n, F f) {
 // key i went.  NT threads per chunk of C keys (C/NT keys per thread).
 // NTS: non-temporal stores of the intermediates (default); plain stores
 // leave them in the Infinity Cache for a round-sized batch to re-read.
-template <int MODE, int NT, int C, int H = 1, bool NTS = true>
+// PERSIST: a grid smaller than the chunk count loops over the chunks with
+// the next chunk's key tiles in flight; otherwise one workgroup per chunk
+// (the default: no cross-chunk state to keep in registers).
+template <int MODE, int NT, int C, int H = 1, bool NTS = true, bool PERSIST = true>
 __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partition_kernel(
     KeyDesc kd, uint32_t L, uint32_t magic, uint32_t R, uint32_t rmagic, uint32_t S, uint32_t nC,
     uint32_t* __restrict__ entries, uint16_t* __restrict__ pos, uint16_t* __restrict__ tab) {
@@ -1245,7 +1248,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
     }
   }
   // grid-stride over chunks (a grid smaller than nC makes the pass persistent)
-  for (uint32_t c = blockIdx.x; c < nC; c += gridDim.x) {
+  for (uint32_t c = blockIdx.x; c < nC; c += PERSIST ? gridDim.x : nC) {
     const uint64_t first = static_cast<uint64_t>(c) * C;
     const uint32_t nk = chunk_keys(c);
     for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
@@ -1255,7 +1258,7 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
       const uint32_t nku = unit_keys(nk, u);
       const uint64_t fu = first + static_cast<uint64_t>(u) * CH;
       if constexpr (kPipe) {
-        const uint32_t cn = c + gridDim.x;
+        const uint32_t cn = PERSIST ? c + gridDim.x : nC;  // the workgroup's next chunk, if any
         const uint64_t nf = u + 1 < H ? fu + CH : static_cast<uint64_t>(cn) * C;
         const uint32_t nn = u + 1 < H ? unit_keys(nk, u + 1) : (cn < nC ? unit_keys(chunk_keys(cn), 0) : 0u);
         hash_chunk_k20_pipe<NT, PER, KB>(kd, fu, nku, nf, nn, tile, h, pre);  // ends with a barrier
@@ -2228,21 +2231,29 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, u
     const char* e = getenv("DLSM_PROBE_PLAIN_STORES");
     return e && atoi(e) != 0;
   }();
+#ifndef DLSM_PPART_PERSIST_ALWAYS
+#define DLSM_PPART_PERSIST_ALWAYS 0  // A/B: the persistent instantiation at every grid size
+#endif
+#define DLSM_PPART(MM, NTS_)                                                                                   \
+  do {                                                                                                         \
+    if (per_cu || DLSM_PPART_PERSIST_ALWAYS)                                                                   \
+      probe_partition_kernel<MM, NT, C, H, NTS_, true><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R),  \
+                                                                        n_slices, nC, entries, pos, tab);      \
+    else                                                                                                       \
+      probe_partition_kernel<MM, NT, C, H, NTS_, false><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), \
+                                                                         n_slices, nC, entries, pos, tab);     \
+  } while (0)
   if (mode == KM_HASH)
-    probe_partition_kernel<KM_HASH, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
-                                                           entries, pos, tab);
+    DLSM_PPART(KM_HASH, true);
   else if (mode == KM_K20 && plain)
-    probe_partition_kernel<KM_K20, NT, C, H, false><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
-                                                                 entries, pos, tab);
+    DLSM_PPART(KM_K20, false);
   else if (mode == KM_K20)
-    probe_partition_kernel<KM_K20, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
-                                                          entries, pos, tab);
+    DLSM_PPART(KM_K20, true);
   else if (mode == KM_K28)
-    probe_partition_kernel<KM_K28, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
-                                                          entries, pos, tab);
+    DLSM_PPART(KM_K28, true);
   else
-    probe_partition_kernel<KM_GENERIC, NT, C, H><<<g, NT, 0, s>>>(keys, L, magic, R, fastmod_magic(R), n_slices, nC,
-                                                              entries, pos, tab);
+    DLSM_PPART(KM_GENERIC, true);
+#undef DLSM_PPART
   return hipGetLastError();
 }
 
