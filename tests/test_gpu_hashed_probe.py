@@ -51,3 +51,38 @@ def test_hashed_probe_mixed_groups(gpu, orc):
     assert np.array_equal(a, b)
     assert np.array_equal(b.reshape(nq, -1)[:50_000].reshape(-1),
                           orc.full_probe(filters, q[: 50_000 * 20], 50_000, nthreads=8))
+
+
+@pytest.mark.parametrize("path", [0, 1, 2])
+def test_hashed_probe_ragged_sizes(gpu, orc, path):
+    """Batches of 1 .. 8,193 hashed lookups (empty, one key, below / at /
+    past one 8,192-key partition chunk) on every path: the same answers as
+    the probe from the keys and the oracle, nothing written past the batch."""
+    import torch
+
+    import dlsm_amd
+
+    n = 100_000
+    filters = [orc.full_build(orc.dbbench_keys(f, 8, n), n) for f in range(8)]
+    fs = gpu.filterset(filters)
+    try:
+        for nq in (1, 7, 64, 8_191, 8_192, 8_193):
+            q = orc.keys_from_values(orc.mt_values(500 + nq, 16 * n, nq))
+            h = torch.from_numpy(dlsm_amd.hash_batch(dlsm_amd.Keys(q, nq, 20)).view(np.int32).copy()).cuda()
+            m = torch.full((nq + 64,), 0x5A, dtype=torch.uint8, device="cuda")
+            gpu.set_path(path)
+            try:
+                gpu.full_probe_hashed_dev(fs, h, m, nq)
+                gpu.sync()
+            finally:
+                gpu.set_path(0)
+            got = m.cpu().numpy()
+            assert np.array_equal(got[:nq], orc.full_probe(filters, q, nq)), (nq, path)
+            assert (got[nq:] == 0x5A).all(), (nq, path)
+        empty = torch.zeros(1, dtype=torch.int32, device="cuda")
+        m0 = torch.full((8,), 0x5A, dtype=torch.uint8, device="cuda")
+        gpu.full_probe_hashed_dev(fs, empty, m0, 0)
+        gpu.sync()
+        assert (m0.cpu().numpy() == 0x5A).all()
+    finally:
+        fs.close()
