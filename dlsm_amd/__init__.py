@@ -105,6 +105,12 @@ def hash_batch(keys: "Keys", out: Optional[np.ndarray] = None, threads: int = 0)
     storage passed as ``out``."""
     if out is None:
         out = np.empty(max(keys.n, 1), dtype=np.uint32)
+    if isinstance(out, np.ndarray):
+        ok = out.itemsize == 4 and out.size >= keys.n and out.flags["C_CONTIGUOUS"]
+    else:  # a torch CPU tensor
+        ok = out.element_size() == 4 and out.numel() >= keys.n and out.is_contiguous() and not out.is_cuda
+    if not ok:
+        raise ValueError("hash_batch: `out` must be contiguous host memory of >= n 4-byte elements")
     ks = keys.c()
     check(lib().dlsm_bloom_hash_batch(C.byref(ks), _ptr(out), threads), "hash_batch")
     return out[: keys.n] if isinstance(out, np.ndarray) else out

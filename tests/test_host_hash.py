@@ -4,6 +4,7 @@ ExtractUserKey for internal keys) on the host's cores, AVX-512 for 20-byte
 keys.  Runs on the CPU (no device is touched); checked against the oracle and
 the golden hashes of the compiled reference."""
 import numpy as np
+import pytest
 
 import dlsm_amd
 
@@ -45,3 +46,13 @@ def test_hash_batch_varlen_internal_and_golden(orc, golden):
     data, offs = orc.pack_var(ks)
     got = dlsm_amd.hash_batch(dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]), len(ks), 0, offs))
     assert [int(x) for x in got] == [int(c["hash"]) for c in cases]
+
+
+def test_hash_batch_rejects_a_short_or_wide_out(orc):
+    import dlsm_amd
+
+    k = orc.dbbench_keys(0, 1, 100)
+    with pytest.raises(ValueError):
+        dlsm_amd.hash_batch(dlsm_amd.Keys(k, 100, 20), out=np.empty(99, dtype=np.uint32))
+    with pytest.raises(ValueError):
+        dlsm_amd.hash_batch(dlsm_amd.Keys(k, 100, 20), out=np.empty(100, dtype=np.uint64))
