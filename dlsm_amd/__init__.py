@@ -129,6 +129,23 @@ def _ptr(x) -> Optional[int]:
     return int(x.data_ptr())
 
 
+def _nbytes(x) -> int:
+    """Bytes of a numpy array or torch tensor (0 for None)."""
+    if x is None:
+        return 0
+    if isinstance(x, np.ndarray):
+        return int(x.nbytes)
+    return int(x.numel()) * int(x.element_size())
+
+
+def _need(x, nbytes: int, what: str):
+    """The binding's guard: a buffer the library writes or reads through a raw
+    pointer must hold at least nbytes (a short device buffer would be written
+    past its end by the kernels)."""
+    if _nbytes(x) < nbytes:
+        raise ValueError(f"{what}: buffer of {_nbytes(x)} bytes, {nbytes} needed")
+
+
 def cu_subset(per_xcd: int, n_cus: int = 256, n_xcds: int = 8) -> list:
     """per_xcd compute units on each XCD under both CU-mask numberings a
     multi-XCD part may use (bit i on XCD i // (n_cus / n_xcds), or on XCD
@@ -164,6 +181,10 @@ class Keys:
     suffix_len: int = 0  # INTERNAL_KEY_TRAILER: internal keys, hashed as ExtractUserKey(key)
 
     def c(self) -> dlsm_keyset:
+        if self.offsets is None:
+            _need(self.data, self.n * self.key_len, "Keys.data")
+        else:
+            _need(self.offsets, 8 * (self.n + 1), "Keys.offsets")
         return dlsm_keyset(_ptr(self.data), _ptr(self.offsets), self.key_len, self.suffix_len, self.n)
 
     @staticmethod
@@ -376,6 +397,7 @@ class Context:
 
     def full_build_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
         """Device keys (torch tensors) -> device slots; asynchronous on this ctx's stream."""
+        _need(out_lens, 8 * len(tables), "full_build_dev out_lens")
         caps = [int(o.numel()) for o in outs]
         jobs = self._jobs(tables, outs, caps)
         check(lib().dlsm_bloom_full_build_dev(self.h, jobs, len(tables), bits_per_key,
@@ -385,6 +407,7 @@ class Context:
         """full_build_dev with its arguments marshalled once: returns a
         zero-argument callable (one ctypes call per invocation; the GIL is
         released inside it), for per-step loops on several host threads."""
+        _need(out_lens, 8 * len(tables), "bind_full_build_dev out_lens")
         caps = [int(o.numel()) for o in outs]
         jobs = self._jobs(tables, outs, caps)
         fn, h, n, lp = lib().dlsm_bloom_full_build_dev, self.h, len(tables), _ptr(out_lens)
@@ -414,6 +437,7 @@ class Context:
 
     def full_build_hashed_dev(self, hash_sets, outs, out_lens, bits_per_key: int = 10):
         """Device form: hash_sets are device uint32 tensors."""
+        _need(out_lens, 8 * len(hash_sets), "full_build_hashed_dev out_lens")
         tables = [Keys(h, int(h.numel()), 4) for h in hash_sets]
         caps = [int(o.numel()) for o in outs]
         jobs = self._jobs(tables, outs, caps)
@@ -520,17 +544,20 @@ class Context:
     def full_probe_hashed_dev(self, fs: FilterSet, hashes, mask, n: Optional[int] = None):
         """Probe from BloomHash values (device uint32 tensor); asynchronous."""
         n = int(hashes.numel()) if n is None else n
+        _need(mask, n * fs.mask_bytes, "full_probe_hashed_dev mask")
         ks = Keys(hashes, n, 4).c()
         check(lib().dlsm_bloom_full_probe_hashed_dev(self.h, fs.h, C.byref(ks), _ptr(mask)),
               "full_probe_hashed_dev")
 
     def full_probe_dev(self, fs: FilterSet, keys: Keys, mask):
+        _need(mask, keys.n * fs.mask_bytes, "full_probe_dev mask")
         ks = keys.c()
         check(lib().dlsm_bloom_full_probe_dev(self.h, fs.h, C.byref(ks), _ptr(mask)),
               "full_probe_dev")
 
     def bind_full_probe_dev(self, fs: FilterSet, keys: Keys, mask):
         """full_probe_dev with its arguments marshalled once (see bind_full_build_dev)."""
+        _need(mask, keys.n * fs.mask_bytes, "bind_full_probe_dev mask")
         ks = keys.c()
         fn, h, fh, kp, mp = lib().dlsm_bloom_full_probe_dev, self.h, fs.h, C.byref(ks), _ptr(mask)
         keep = (ks, fs, keys, mask)
@@ -554,6 +581,7 @@ class Context:
         return [outs[j][: lens[j]].tobytes() for j in range(n)]
 
     def legacy_build_dev(self, tables: Sequence[Keys], outs, out_lens, bits_per_key: int = 10):
+        _need(out_lens, 8 * len(tables), "legacy_build_dev out_lens")
         caps = [int(o.numel()) for o in outs]
         jobs = self._jobs(tables, outs, caps)
         check(lib().dlsm_bloom_legacy_build_dev(self.h, jobs, len(tables), bits_per_key,
@@ -568,6 +596,8 @@ class Context:
         return out[: keys.n]
 
     def legacy_probe_dev(self, filt_dev, length: int, keys: Keys, out):
+        _need(filt_dev, length, "legacy_probe_dev filter")
+        _need(out, keys.n, "legacy_probe_dev out")
         ks = keys.c()
         check(lib().dlsm_bloom_legacy_probe_dev(self.h, _ptr(filt_dev), length, C.byref(ks),
                                                 _ptr(out)), "legacy_probe_dev")
