@@ -695,21 +695,21 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     reference does it (BloomHash in AddKey and in KeyMayMatch,
     full_filter_block.cc:45,271).  Keys start in pinned host memory; filters
     and masks end in pinned host memory.  Two feeds run at once:
-      - host-hashed lookups: the host's cores hash a chunk
-        (dlsm_bloom_hash_batch, inside the timed region), 4 B per key go H2D,
-        the GPU probes from the hashes (dlsm_bloom_full_probe_hashed_dev);
-        the host hashes chunk i + 1 while chunk i's copy and kernels run
-        (a pinned hash slot per lookup: no staging to wait for);
-      - raw keys: the build's tables and the first `raw` lookups go H2D as
-        20-byte keys on a second context and stream and are hashed on the GPU
-        (the DMA engines read them, not the host's cores).
+      - host-hashed keys: the host's cores hash them (dlsm_bloom_hash_batch,
+        inside the timed region) -- the build's tables first (one hashed
+        batch build, dlsm_bloom_full_build_hashed_dev), then lookups in
+        chunks (hashed probe, dlsm_bloom_full_probe_hashed_dev), each chunk's
+        4 B/key copy and kernels running while the host hashes the next (a
+        pinned hash slot per key: no staging to wait for);
+      - raw keys: the remaining tables and lookups go H2D as 20-byte keys on
+        a second context and stream, hashed on the GPU (the DMA engines read
+        them, not the host's cores).
     Every key is read from host DRAM once either way (20 B); the split puts
-    as many keys on the host's cores as its DRAM read rate allows while the
-    PCIe link carries the rest: `raw` is chosen from the hash rate and the H2D
-    rate measured in the warm-up (time on the cores = time on the link).
-    D2H copies run on a third stream (PCIe is full duplex).  `ref` =
-    (filters, mask) of the device-resident run: the outputs are checked
-    against them."""
+    as many keys on the host's cores as their hash rate allows while the PCIe
+    link carries the rest: it is set from the hash rate and the H2D rate
+    measured in the warm-up (time on the cores = time on the link).  D2H
+    copies run on a third stream (PCIe is full duplex).  `ref` = (filters,
+    mask) of the device-resident run: the outputs are checked against them."""
     import numpy as np
     import torch
 
@@ -718,13 +718,15 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     T, N, Q = len(tables), tables[0].n, qk.n
     mb = fs.mask_bytes
     h_tabs = [t.data.cpu().pin_memory() for t in tables]
+    tab_np = [h.numpy() for h in h_tabs]
     h_q = qk.data.cpu().pin_memory()
     q_np = h_q.numpy()
-    # one pinned slot per lookup's hash: the host never waits for a copy to
-    # free its staging (the raw feed's copies hold the link for most of the step)
-    hb = torch.empty(Q, dtype=torch.int32).pin_memory()
+    hb = torch.empty(Q, dtype=torch.int32).pin_memory()     # lookups' hashes
     hb_np = hb.numpy()
+    hbt = torch.empty(T * N, dtype=torch.int32).pin_memory()  # tables' hashes
+    hbt_np = hbt.numpy()
     db = torch.empty(Q, dtype=torch.int32, device=dev)
+    dbt = torch.empty(T * N, dtype=torch.int32, device=dev)
     d_tabs = [torch.empty_like(t.data) for t in tables]
     d_q = torch.empty_like(qk.data)
     outs = [torch.zeros(dlsm_amd.full_size(t.n, bpk)[0] + 16, dtype=torch.uint8, device=dev) for t in tables]
@@ -738,26 +740,45 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     ctx_raw = dlsm_amd.Context(dev.index or 0)
     ctx_raw.set_stream(s_raw)
 
-    def one_step(raw):
-        """raw: lookups [0, raw) go as keys, [raw, Q) hashed on the host."""
+    def to_host(lo_t, hi_t, lo_q, hi_q, st):
+        """D2H of tables [lo_t, hi_t) and lookups [lo_q, hi_q), behind st's work."""
+        done = torch.cuda.Event()
+        done.record(st)
+        s_out.wait_event(done)
+        with torch.cuda.stream(s_out):
+            for s_ in range(lo_t, hi_t):
+                h_outs[s_].copy_(outs[s_], non_blocking=True)
+            if hi_t > lo_t:
+                h_lens[lo_t:hi_t].copy_(lens[lo_t:hi_t], non_blocking=True)
+            if hi_q > lo_q:
+                h_mask[lo_q * mb:hi_q * mb].copy_(mask[lo_q * mb:hi_q * mb], non_blocking=True)
+
+    def one_step(raw_t, raw_q):
+        """Tables [0, raw_t) and lookups [0, raw_q) go as keys; tables
+        [raw_t, T) and lookups [raw_q, Q) are hashed on the host."""
         hash_s = 0.0
         with torch.cuda.stream(s_raw):  # the raw feed, queued up front
-            for d, h in zip(d_tabs, h_tabs):
-                d.copy_(h, non_blocking=True)
-            if raw:
-                d_q[: raw * 20].copy_(h_q[: raw * 20], non_blocking=True)
-        ctx_raw.full_build_dev([dlsm_amd.Keys(d, t.n, 20) for d, t in zip(d_tabs, tables)], outs, lens, bpk)
-        if raw:
-            ctx_raw.full_probe_dev(fs, dlsm_amd.Keys(d_q[: raw * 20], raw, 20), mask[: raw * mb])
-        raw_done = torch.cuda.Event()
-        raw_done.record(s_raw)
-        s_out.wait_event(raw_done)
-        with torch.cuda.stream(s_out):
-            for h, o in zip(h_outs, outs):
-                h.copy_(o, non_blocking=True)
-            h_lens.copy_(lens, non_blocking=True)
-            h_mask[: raw * mb].copy_(mask[: raw * mb], non_blocking=True)
-        for lo in range(raw, Q, chunk_keys):
+            for s_ in range(raw_t):
+                d_tabs[s_].copy_(h_tabs[s_], non_blocking=True)
+            if raw_q:
+                d_q[: raw_q * 20].copy_(h_q[: raw_q * 20], non_blocking=True)
+        if raw_t:
+            ctx_raw.full_build_dev([dlsm_amd.Keys(d_tabs[s_], N, 20) for s_ in range(raw_t)], outs[:raw_t],
+                                   lens[:raw_t], bpk)
+        if raw_q:
+            ctx_raw.full_probe_dev(fs, dlsm_amd.Keys(d_q[: raw_q * 20], raw_q, 20), mask[: raw_q * mb])
+        to_host(0, raw_t, 0, raw_q, s_raw)
+        if raw_t < T:  # the hashed tables: one batched build from their hashes
+            t0 = time.perf_counter()
+            for s_ in range(raw_t, T):
+                dlsm_amd.hash_batch(dlsm_amd.Keys(tab_np[s_], N, 20), out=hbt_np[s_ * N:(s_ + 1) * N])
+            hash_s += time.perf_counter() - t0
+            with torch.cuda.stream(stream):
+                dbt[raw_t * N:].copy_(hbt[raw_t * N:], non_blocking=True)
+            ctx.full_build_hashed_dev([dbt[s_ * N:(s_ + 1) * N] for s_ in range(raw_t, T)], outs[raw_t:],
+                                      lens[raw_t:], bpk)
+            to_host(raw_t, T, 0, 0, stream)
+        for lo in range(raw_q, Q, chunk_keys):
             hi = min(Q, lo + chunk_keys)
             n = hi - lo
             t0 = time.perf_counter()
@@ -766,52 +787,57 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
             with torch.cuda.stream(stream):
                 db[lo:hi].copy_(hb[lo:hi], non_blocking=True)
             ctx.full_probe_hashed_dev(fs, db[lo:hi], mask[lo * mb:hi * mb], n)
-            done = torch.cuda.Event()
-            done.record(stream)
-            s_out.wait_event(done)
-            with torch.cuda.stream(s_out):
-                h_mask[lo * mb:hi * mb].copy_(mask[lo * mb:hi * mb], non_blocking=True)
+            to_host(0, 0, lo, hi, stream)
         stream.synchronize()
         s_raw.synchronize()
         s_out.synchronize()
         return hash_s
 
-    # warm-up: workspaces, pool threads, and the two rates the split is set by
-    raw0 = min(chunk_keys, Q // 2)
-    hs = one_step(raw0)
-    hash_rate = (Q - raw0) / max(hs, 1e-9)  # keys/s on the host's cores
+    # warm-up: workspaces, pool threads, and the two rates the split is set
+    # by (half the lookups and every table hashed on the host)
+    hs = one_step(0, Q // 2)
+    hash_rate = (T * N + Q - Q // 2) / max(hs, 1e-9)  # keys/s on the host's cores
+    one_step(T, Q)  # the raw feed's workspaces
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(s_raw):
         d_q.copy_(h_q, non_blocking=True)
     s_raw.synchronize()
     h2d_Bps = h_q.numel() / (time.perf_counter() - t0)
-    # raw lookups r: (Q - r) / hash_rate = (20 (T N + r) + 4 (Q - r)) / h2d_Bps
-    r = (Q / hash_rate - (20 * T * N + 4 * Q) / h2d_Bps) / (1 / hash_rate + 16 / h2d_Bps)
-    raw = int(min(Q, max(0, round(r / 4096) * 4096)))
-    one_step(raw)
+    # host-hashed keys H of K: H / hash_rate = (20 (K - H) + 4 H) / h2d_Bps;
+    # the tables are hashed first (their build is one call), then lookups
+    K = T * N + Q
+    H = (20 * K / h2d_Bps) / (1 / hash_rate + 16 / h2d_Bps)
+    H = min(K, max(0.0, H))
+    if H >= T * N:
+        raw_t, raw_q = 0, int(min(Q, max(0, round((K - H) / 4096) * 4096)))
+    else:
+        raw_t, raw_q = T - int(round(H / N)), Q
+    one_step(raw_t, raw_q)
     times = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        one_step(raw)
+        one_step(raw_t, raw_q)
         times.append(time.perf_counter() - t0)
     dt = float(np.median(times))
     L = h_lens.numpy()
     ref_filters, ref_mask = ref
     ok = (all(h_outs[s_][: int(L[s_])].numpy().tobytes() == ref_filters[s_] for s_ in range(T))
           and bool(np.array_equal(h_mask.numpy(), ref_mask)))
-    nk = T * N + Q
     ctx_raw.close()
-    return {"mkeys_s": round(nk / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
+    hashed = (T - raw_t) * N + (Q - raw_q)
+    return {"mkeys_s": round(K / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
             "ms_per_step_reps": [round(x * 1e3, 3) for x in times],
-            "host_hashed_keys": Q - raw, "raw_keys": T * N + raw,
+            "host_hashed_keys": hashed, "raw_keys": K - hashed,
+            "host_hashed_tables": T - raw_t, "host_hashed_lookups": Q - raw_q,
             "host_hash_gkeys_s": round(hash_rate / 1e9, 3), "h2d_GBs": round(h2d_Bps / 1e9, 1),
             "host_hash_threads": "all usable cores (dlsm_bloom_hash_batch pool)",
             "chunk_keys": chunk_keys, "h2d_bytes_per_key": {"host_hashed": 4, "raw": 20},
             "matches_device_resident": ok,
-            "note": ("host BloomHash (timed) of the lookups the host's DRAM rate allows, 4 B/key H2D, hashed probe; "
-                     "the build's tables and the other lookups H2D as 20-byte keys on a second stream, hashed on "
-                     "the GPU; D2H filters/masks on a third stream; pinned host buffers")}
+            "note": ("host BloomHash (timed) of as many keys as the host's cores keep up with -- the tables "
+                     "first (hashed batch build), then lookups (hashed probe) -- 4 B/key H2D; the other keys "
+                     "H2D as 20-byte keys on a second context and stream, hashed on the GPU; D2H filters/masks "
+                     "on a third stream; pinned host buffers")}
 
 
 def host_cores() -> int:
