@@ -804,15 +804,8 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
         d_q.copy_(h_q, non_blocking=True)
     s_raw.synchronize()
     h2d_Bps = h_q.numel() / (time.perf_counter() - t0)
-    # host-hashed keys H of K: H / hash_rate = (20 (K - H) + 4 H) / h2d_Bps;
-    # the tables are hashed first (their build is one call), then lookups
+    raw_t, raw_q = e2e_split(T, N, Q, hash_rate, h2d_Bps)
     K = T * N + Q
-    H = (20 * K / h2d_Bps) / (1 / hash_rate + 16 / h2d_Bps)
-    H = min(K, max(0.0, H))
-    if H >= T * N:
-        raw_t, raw_q = 0, int(min(Q, max(0, round((K - H) / 4096) * 4096)))
-    else:
-        raw_t, raw_q = T - int(round(H / N)), Q
     one_step(raw_t, raw_q)
     times = []
     for _ in range(reps):
@@ -838,6 +831,20 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
                      "first (hashed batch build), then lookups (hashed probe) -- 4 B/key H2D; the other keys "
                      "H2D as 20-byte keys on a second context and stream, hashed on the GPU; D2H filters/masks "
                      "on a third stream; pinned host buffers")}
+
+
+def e2e_split(T, N, Q, hash_rate, h2d_Bps):
+    """How many of a step's keys e2e_hashed sends raw: (raw tables, raw
+    lookups).  H host-hashed keys of K = T N + Q balance the host's cores
+    against the link: H / hash_rate = (20 (K - H) + 4 H) / h2d_Bps.  The
+    tables are hashed first (their build is one call), then lookups; raw
+    lookups are rounded to 4,096 keys."""
+    K = T * N + Q
+    H = (20 * K / h2d_Bps) / (1 / hash_rate + 16 / h2d_Bps)
+    H = min(K, max(0.0, H))
+    if H >= T * N:
+        return 0, int(min(Q, max(0, round((K - H) / 4096) * 4096)))
+    return T - int(round(H / N)), Q
 
 
 def host_cores() -> int:

@@ -84,3 +84,24 @@ def test_threads_line_schema_per_gpu():
     assert line["roofline"]["kernel"].startswith("probe pass of the slowest GPU")
     assert line["roofline"]["frac"] == per_gpu[-1]["probe_frac"]
     assert line["config"]["gpu_tables"][1] == list(range(1, T, n_gpu))
+
+
+def test_e2e_split_balances_cores_and_link():
+    """e2e_hashed's split: the host-hashed keys take as long on the host's
+    cores as the rest take on the link; tables are hashed before lookups."""
+    b = _bench()
+    T, N, Q, bw = 16, 1_600_000, 100_000_000, 57e9
+    K = T * N + Q
+    for rate in (2e9, 4e9, 8.3e9, 50e9):
+        raw_t, raw_q = b.e2e_split(T, N, Q, rate, bw)
+        assert 0 <= raw_t <= T and 0 <= raw_q <= Q
+        hashed = (T - raw_t) * N + (Q - raw_q)
+        if raw_t:  # lookups are hashed only once every table is
+            assert raw_q == Q
+        cores = hashed / rate
+        link = (20 * (K - hashed) + 4 * hashed) / bw
+        if hashed == K:  # the host outruns the link even at 4 B/key: hash everything
+            assert cores <= link
+        else:
+            assert abs(cores - link) <= max(N, 4096) * (1 / rate + 16 / bw) + 1e-9, (rate, cores, link)
+    assert b.e2e_split(T, N, Q, 1e15, bw) == (0, 0)  # a host that hashes everything
