@@ -2220,14 +2220,16 @@ static hipError_t probe_partition_as(KeyDesc keys, uint32_t L, uint32_t magic, u
   // overlapped step -4 % (the hardware's dispatcher keeps every CU's phases
   // mixed, with no tail of long-running workgroups and room for the build's
   // workgroups beside them); neutral at the N = 4 / 8 shares.
-  // 28-byte internal keys keep the persistent grid (2 per CU): their
-  // one-workgroup-per-chunk form spills more and measured 6 % slower
-  // (`profiles/r04_z_internal_keys_grid_ab.txt`).
+  // Only 20-byte keys take one workgroup per chunk by default: 28-byte
+  // internal keys (their one-per-chunk form spills more: 6 % slower,
+  // `profiles/r04_z_internal_keys_grid_ab.txt`) and hashed lookups (4 %
+  // slower, `r04_z4_hashed_probe_grid_ab.txt`) keep the persistent grid, as
+  // do variable-length keys (round 3's default, not re-measured).
   static const int per_cu_env = [] {
     const char* e = getenv("DLSM_PART_GRID_PER_CU");
     return e ? atoi(e) : -1;
   }();
-  const uint32_t per_cu = per_cu_env >= 0 ? static_cast<uint32_t>(per_cu_env) : (mode == KM_K28 ? 2u : 0u);
+  const uint32_t per_cu = per_cu_env >= 0 ? static_cast<uint32_t>(per_cu_env) : (mode == KM_K20 ? 0u : 2u);
   const uint32_t g = per_cu ? std::min(nC, per_cu * (cus ? cus : device_cus())) : nC;
   // $DLSM_PROBE_PLAIN_STORES=1: plain (Infinity-Cache-allocating) intermediate
   // stores, for round-sized batches (A/B knob; K20 keys only)
