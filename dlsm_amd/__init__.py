@@ -35,6 +35,7 @@ INTERNAL_KEY_TRAILER = 8  # dlsm_keyset.suffix_len for internal keys (db/dbforma
 SELECT_FLUSH, SELECT_COMPACTION = 0, 1  # dlsm_internal_keys_select_dev policies
 OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_option
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
+OPT_FAULT_INJECT = 7  # test hook: builds / probes on the context return -value
 
 
 def lib():
@@ -185,6 +186,11 @@ class Keys:
             _need(self.data, self.n * self.key_len, "Keys.data")
         else:
             _need(self.offsets, 8 * (self.n + 1), "Keys.offsets")
+            # host offsets: the data must also hold the bytes they index (key
+            # n-1 ends at offsets[n]); device offsets are not read back here (a
+            # synchronising copy per call), the caller vouches for them
+            if isinstance(self.offsets, np.ndarray) and self.n:
+                _need(self.data, int(self.offsets[self.n]), "Keys.data")
         return dlsm_keyset(_ptr(self.data), _ptr(self.offsets), self.key_len, self.suffix_len, self.n)
 
     @staticmethod

@@ -73,6 +73,9 @@ SIGNATURES = [
     ("dlsm_ctx_destroy", C.c_int, [_VP]),
     ("dlsm_thread_ctx", C.c_int, [C.POINTER(_VP)]),
     ("dlsm_thread_ctx_bind", C.c_int, [_VP]),
+    ("dlsm_thread_ctx_stats", C.c_int, [_U64P, _U64P, _U64P]),
+    ("dlsm_fallback_note", None, [_VP]),
+    ("dlsm_fallback_stats", C.c_int, [_VP, _U64P, _U64P]),
     ("dlsm_ctx_set_stream", C.c_int, [_VP, _VP]),
     ("dlsm_ctx_stream", _VP, [_VP]),
     ("dlsm_ctx_sync", C.c_int, [_VP]),

@@ -108,6 +108,8 @@ struct dlsm_ctx {
   int probe_lgr = 8;         // log2 stacked lines per probe slice (7: 64 KiB, 8: 128 KiB of LDS)
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
+  int fault = 0;              // DLSM_OPT_FAULT_INJECT: > 0 -> builds / probes return -fault
+  std::atomic<uint64_t> fallbacks{0};  // dlsm_fallback_note: host re-runs of this context's failed calls
   // build workspace
   DevBuf<uint32_t> entries;
   DevBuf<uint16_t> tab;  // chunk-major bucket offsets
@@ -456,13 +458,41 @@ int dlsm_device_count(int* n) {
 
 }  // extern "C"
 namespace {
-// Per-thread contexts (dlsm_thread_ctx): owned = created here, destroyed at
-// the thread's exit; bound = the caller's (dlsm_thread_ctx_bind), never freed here.
+// Per-thread contexts (dlsm_thread_ctx): owned = handed out here, returned to
+// a per-device free list at the thread's exit; bound = the caller's
+// (dlsm_thread_ctx_bind), never touched here.  dLSM starts a std::thread per
+// subcompaction (db/db_impl.cc:3373-3386): with the free list a new thread
+// takes a context a finished one left -- its stream, page-locked blocks,
+// events and grown device workspaces -- instead of paying their creation
+// (hipHostMalloc takes a process-wide lock) and teardown per compaction.
+// The list is never freed: contexts outlive every thread, so a builder that
+// outlives its thread still holds a live context, and nothing is destroyed
+// during static destruction, after the HIP runtime may be gone.
+struct CtxPool {
+  std::mutex m;
+  std::map<int, std::vector<dlsm_ctx*>> free;  // device -> idle contexts
+  uint64_t created = 0, reused = 0;
+};
+CtxPool& ctx_pool() {
+  static CtxPool* p = new CtxPool();  // intentionally leaked (see above)
+  return *p;
+}
+// The scheduling options a context starts with; a recycled context gets them
+// back (a thread may have changed them, e.g. a builder's BUILD_EXACT).
+struct CtxOpts {
+  int path, build_groups;
+  uint64_t probe_round;
+  int probe_lgc, probe_lgr, build_exact;
+  bool probe_serial;
+};
+std::mutex g_opts_m;
+std::map<const dlsm_ctx*, CtxOpts> g_opts;  // creation options of pooled contexts
+void ctx_pool_put(dlsm_ctx* c);
 struct ThreadCtx {
   dlsm_ctx* owned = nullptr;
   dlsm_ctx* bound = nullptr;
   ~ThreadCtx() {
-    if (owned) dlsm_ctx_destroy(owned);
+    if (owned) ctx_pool_put(owned);
   }
 };
 ThreadCtx& thread_ctx_slot() {
@@ -470,6 +500,7 @@ ThreadCtx& thread_ctx_slot() {
   return t;
 }
 std::atomic<unsigned> g_thread_ctx_next{0};
+std::atomic<uint64_t> g_fallbacks{0};  // dlsm_fallback_note, process-wide
 }  // namespace
 extern "C" {
 
@@ -487,7 +518,25 @@ int dlsm_thread_ctx(dlsm_ctx** out) {
       return DLSM_E_DEVICE;
     }
     const int dev = static_cast<int>(g_thread_ctx_next.fetch_add(1) % static_cast<unsigned>(n));
-    DLSM_CHECK(dlsm_ctx_create(dev, &t.owned));
+    CtxPool& p = ctx_pool();
+    {
+      std::lock_guard<std::mutex> lk(p.m);
+      auto& v = p.free[dev];
+      if (!v.empty()) {
+        t.owned = v.back();
+        v.pop_back();
+        p.reused++;
+      }
+    }
+    if (!t.owned) {
+      DLSM_CHECK(dlsm_ctx_create(dev, &t.owned));
+      const CtxOpts o{t.owned->path, t.owned->build_groups, t.owned->probe_round, t.owned->probe_lgc,
+                      t.owned->probe_lgr, t.owned->build_exact, t.owned->probe_serial};
+      std::lock_guard<std::mutex> lk(p.m);
+      p.created++;
+      std::lock_guard<std::mutex> lo(g_opts_m);
+      g_opts[t.owned] = o;
+    }
   }
   *out = t.owned;
   return DLSM_OK;
@@ -495,6 +544,28 @@ int dlsm_thread_ctx(dlsm_ctx** out) {
 
 int dlsm_thread_ctx_bind(dlsm_ctx* ctx) {
   thread_ctx_slot().bound = ctx;
+  return DLSM_OK;
+}
+
+int dlsm_thread_ctx_stats(uint64_t* created, uint64_t* reused, uint64_t* idle) {
+  CtxPool& p = ctx_pool();
+  std::lock_guard<std::mutex> lk(p.m);
+  uint64_t n = 0;
+  for (auto& kv : p.free) n += kv.second.size();
+  if (created) *created = p.created;
+  if (reused) *reused = p.reused;
+  if (idle) *idle = n;
+  return DLSM_OK;
+}
+
+void dlsm_fallback_note(dlsm_ctx* ctx) {
+  g_fallbacks.fetch_add(1, std::memory_order_relaxed);
+  if (ctx) ctx->fallbacks.fetch_add(1, std::memory_order_relaxed);
+}
+
+int dlsm_fallback_stats(const dlsm_ctx* ctx, uint64_t* ctx_count, uint64_t* process_count) {
+  if (ctx_count) *ctx_count = ctx ? ctx->fallbacks.load(std::memory_order_relaxed) : 0;
+  if (process_count) *process_count = g_fallbacks.load(std::memory_order_relaxed);
   return DLSM_OK;
 }
 
@@ -595,6 +666,42 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   return DLSM_OK;
 }
 
+}  // extern "C"
+namespace {
+// A thread's context back to its device's free list: drained, its stream and
+// partition stream reset to its own, its scheduling options to their
+// creation values, fault injection off.
+void ctx_pool_put(dlsm_ctx* c) {
+  {
+    DeviceGuard g(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->pstream) (void)hipStreamSynchronize(c->pstream);
+  }
+  c->stream = c->own;
+  c->pstream = nullptr;
+  c->pcus = 0;
+  c->fault = 0;
+  {
+    std::lock_guard<std::mutex> lo(g_opts_m);
+    auto it = g_opts.find(c);
+    if (it != g_opts.end()) {
+      const CtxOpts& o = it->second;
+      c->path = o.path;
+      c->build_groups = o.build_groups;
+      c->probe_round = o.probe_round;
+      c->probe_lgc = o.probe_lgc;
+      c->probe_lgr = o.probe_lgr;
+      c->build_exact = o.build_exact;
+      c->probe_serial = o.probe_serial;
+    }
+  }
+  CtxPool& p = ctx_pool();
+  std::lock_guard<std::mutex> lk(p.m);
+  p.free[c->device].push_back(c);
+}
+}  // namespace
+extern "C" {
+
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* s) {
   if (!ctx) return DLSM_E_ARG;
   ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
@@ -671,6 +778,10 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > 1) return DLSM_E_ARG;
       ctx->probe_serial = value != 0;
       return DLSM_OK;
+    case DLSM_OPT_FAULT_INJECT:
+      if (value > static_cast<uint64_t>(-DLSM_E_BUSY)) return DLSM_E_ARG;
+      ctx->fault = static_cast<int>(value);
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -686,6 +797,7 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_PROBE_SLICE_LG: *value = static_cast<uint64_t>(ctx->probe_lgr); return DLSM_OK;
     case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
     case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
+    case DLSM_OPT_FAULT_INJECT: *value = static_cast<uint64_t>(ctx->fault); return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -893,6 +1005,7 @@ bool is_hash_set(const dlsm_keyset& k) {
 int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
                         uint64_t* out_len_dev, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
   const int k = full_num_probes(bits_per_key);
@@ -1117,6 +1230,7 @@ bool full_build_sliced(const dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jo
 int full_build_host_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
                          uint64_t* out_len, bool hashed) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
   std::vector<const dlsm_keyset*> sets(n_jobs);
@@ -1644,6 +1758,7 @@ namespace {
 int full_probe_dev_impl(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys, uint8_t* mask_dev,
                         bool hashed) {
   if (!ctx || !fs || !keys) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   if (fs->device != ctx->device) return DLSM_E_ARG;
   DLSM_CHECK(validate_keyset(*keys));
   if (hashed && !is_hash_set(*keys)) return DLSM_E_ARG;
@@ -1743,6 +1858,7 @@ int dlsm_bloom_full_probe_hashed_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, co
 int dlsm_bloom_full_probe(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keyset* keys,
                           uint8_t* mask) {
   if (!ctx || !fs || !keys) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   DLSM_CHECK(validate_keyset(*keys));
   if (keys->n == 0) return DLSM_OK;
   if (!mask) return DLSM_E_ARG;
@@ -2097,6 +2213,7 @@ int choose_legacy_tps_lg(const std::vector<uint32_t>& n_tiles) {
 int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs,
                                 int bits_per_key, uint64_t* out_len_dev) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
@@ -2170,7 +2287,9 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
                                   ctx->ltab.p, tps_lg, s));
     return DLSM_OK;
   }
-  if (ctx->path == 2) return DLSM_E_ARG;  // sliced forced, but the batch does not fit it
+  // path 2 (sliced forced) with a batch the tiled kernels cannot take
+  // (k > kLegacyKmaxB, i.e. bits_per_key >= 14, or too many tiles): the
+  // direct kernel builds it -- the same bytes
   // Direct path: global atomics into an aligned workspace, then copies to the slots.
   DLSM_CHECK(ctx->st_filter.ensure(ws + 256));
   DLSM_TRY(hipMemsetAsync(ctx->st_filter.p, 0, ws, s));
@@ -2212,6 +2331,7 @@ int dlsm_bloom_legacy_build_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n
 int dlsm_bloom_legacy_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
                             uint64_t* out_len) {
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len))) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   if (n_jobs == 0) return DLSM_OK;
   DeviceGuard g(ctx->device);
   std::vector<const dlsm_keyset*> sets(n_jobs);
@@ -2250,6 +2370,7 @@ int dlsm_bloom_legacy_build(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_job
 int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64_t len,
                                 const dlsm_keyset* keys, uint8_t* out_dev) {
   if (!ctx || !keys) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   DLSM_CHECK(validate_keyset(*keys));
   if (keys->n == 0) return DLSM_OK;
   if (!out_dev) return DLSM_E_ARG;
@@ -2279,6 +2400,7 @@ int dlsm_bloom_legacy_probe_dev(dlsm_ctx* ctx, const uint8_t* filter_dev, uint64
 int dlsm_bloom_legacy_probe(dlsm_ctx* ctx, const uint8_t* filter, uint64_t len,
                             const dlsm_keyset* keys, uint8_t* out) {
   if (!ctx || !keys) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   DLSM_CHECK(validate_keyset(*keys));
   if (keys->n == 0) return DLSM_OK;
   if (!out) return DLSM_E_ARG;

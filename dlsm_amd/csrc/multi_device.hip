@@ -58,11 +58,11 @@ int drain(const dlsm_device_work& w) {
   return s;
 }
 
-}  // namespace
-
-extern "C" int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n, int bits_per_key, int steps,
-                                           int warmup, int event_every, double* wall_seconds, float* pass_ms,
-                                           double* device_seconds) {
+// instrument_all: every device records its pass events (dlsm_multi_device_run_timed);
+// else only entry 0 does (dlsm_multi_device_run[_sampled], whose header promises
+// entry 0's passes): the other devices' steps keep their build / probe overlap.
+int run_impl(const dlsm_device_work* work, int n, int bits_per_key, int steps, int warmup, int event_every,
+             double* wall_seconds, float* pass_ms, double* device_seconds, bool instrument_all) {
   if (!work || n < 1 || steps < 1 || warmup < 0 || !wall_seconds || event_every < 1) return DLSM_E_ARG;
   for (int d = 0; d < n; d++) {
     const dlsm_device_work& w = work[d];
@@ -88,7 +88,7 @@ extern "C" int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n, 
       // probes before it, its probe after its build, the next build after its
       // probe -- so the events time each pass by itself (the roofline's
       // kernel time), not beside the other.
-      const bool events = pass_ms && st == DLSM_OK;
+      const bool events = pass_ms && st == DLSM_OK && (instrument_all || d == 0);
       std::vector<hipEvent_t> ev;
       hipEvent_t gate = nullptr;
       if (events) {
@@ -156,12 +156,22 @@ extern "C" int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n, 
   return DLSM_OK;
 }
 
+}  // namespace
+
+extern "C" int dlsm_multi_device_run_timed(const dlsm_device_work* work, int n, int bits_per_key, int steps,
+                                           int warmup, int event_every, double* wall_seconds, float* pass_ms,
+                                           double* device_seconds) {
+  if (pass_ms && n > 0 && steps > 0)
+    for (size_t i = 0; i < 2 * static_cast<size_t>(steps) * n; i++) pass_ms[i] = -1.f;
+  return run_impl(work, n, bits_per_key, steps, warmup, event_every, wall_seconds, pass_ms, device_seconds, true);
+}
+
 extern "C" int dlsm_multi_device_run_sampled(const dlsm_device_work* work, int n, int bits_per_key, int steps,
                                              int warmup, int event_every, double* wall_seconds, float* pass_ms) {
   if (n < 1 || steps < 1) return DLSM_E_ARG;
   std::vector<float> all(pass_ms ? 2 * static_cast<size_t>(steps) * n : 0);
-  const int st = dlsm_multi_device_run_timed(work, n, bits_per_key, steps, warmup, event_every, wall_seconds,
-                                             pass_ms ? all.data() : nullptr, nullptr);
+  const int st = run_impl(work, n, bits_per_key, steps, warmup, event_every, wall_seconds,
+                          pass_ms ? all.data() : nullptr, nullptr, false);
   if (pass_ms && st == DLSM_OK)
     for (int i = 0; i < 2 * steps; i++) pass_ms[i] = all[i];  // device 0's
   return st;

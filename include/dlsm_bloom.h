@@ -118,15 +118,29 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx);
 int dlsm_ctx_set_stream(dlsm_ctx* ctx, void* hip_stream);
 void* dlsm_ctx_stream(dlsm_ctx* ctx);
 /* The calling thread's context: the one bound with dlsm_thread_ctx_bind, else
- * one the library creates on the thread's first call -- on device (i mod
- * device count) for the i-th thread that asks -- and destroys when the thread
- * exits.  dLSM runs each TableBuilder on one thread (flush / compaction /
- * subcompaction threads, include/TimberSaw/options.h:73-78), so a
- * FullFilterBlockBuilder with the reference's (ibv_mr*, bits_per_key)
- * signature (table/full_filter_block.h:35) takes its context from here. */
+ * one the library hands out on the thread's first call -- on device (i mod
+ * device count) for the i-th thread that asks -- and takes back when the
+ * thread exits.  Returned contexts wait in a per-device free list (drained,
+ * their stream and scheduling options reset) for the next new thread: dLSM
+ * starts a std::thread per subcompaction (db/db_impl.cc:3373-3386), which then
+ * reuses a context instead of creating one.  dLSM runs each TableBuilder on
+ * one thread (flush / compaction / subcompaction threads,
+ * include/TimberSaw/options.h:73-78), so a FullFilterBlockBuilder with the
+ * reference's (ibv_mr*, bits_per_key) signature (table/full_filter_block.h:35)
+ * takes its context from here. */
 int dlsm_thread_ctx(dlsm_ctx** out);
 /* Bind a context the caller owns (NULL: unbind) as the calling thread's. */
 int dlsm_thread_ctx_bind(dlsm_ctx* ctx);
+/* Thread contexts created so far, handed out again from the free list, and
+ * idle in the free list now. */
+int dlsm_thread_ctx_stats(uint64_t* created, uint64_t* reused, uint64_t* idle);
+/* Host fallbacks.  The C++ adapter (dlsm_bloom_adapter.hpp) answers a call
+ * the GPU failed (device error, out of memory, injected fault, no device) with
+ * the reference's own host loop -- so Finish never emits a 0-byte filter the
+ * reference reader would exit on -- and records every such re-run here: on
+ * the context (if any) and process-wide.  Parity tests assert both stay 0. */
+void dlsm_fallback_note(dlsm_ctx* ctx);
+int dlsm_fallback_stats(const dlsm_ctx* ctx, uint64_t* ctx_count, uint64_t* process_count);
 /* The device a context runs on (-1 for NULL). */
 int dlsm_ctx_device(const dlsm_ctx* ctx);
 int dlsm_ctx_sync(dlsm_ctx* ctx);
@@ -173,7 +187,10 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             count then takes a slower per-slice re-hash fallback)
  *   DLSM_OPT_PROBE_ROUND_SERIAL 1: probe rounds run one after another on the context
  *                             stream (one buffer set) instead of pipelined over two
- *                             streams (default 0, or $DLSM_PROBE_SERIAL) */
+ *                             streams (default 0, or $DLSM_PROBE_SERIAL)
+ *   DLSM_OPT_FAULT_INJECT     test hook: v > 0 makes every build and probe call on the
+ *                             context return -v (4 = DLSM_E_DEVICE, 5 = DLSM_E_NOMEM)
+ *                             before touching the device; 0 (default) off */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
@@ -181,6 +198,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_PROBE_SLICE_LG 4
 #define DLSM_OPT_BUILD_EXACT 5
 #define DLSM_OPT_PROBE_ROUND_SERIAL 6
+#define DLSM_OPT_FAULT_INJECT 7
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 /* The current value of an option (so a caller can restore it). */
 int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);

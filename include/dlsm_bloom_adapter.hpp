@@ -26,14 +26,24 @@
 // here can be stored in Options::filter_policy (options.h:185-187).
 //
 // No exceptions and no RTTI (the reference builds with -fno-exceptions
-// -fno-rtti): failures are reported through status().  All compute runs on
-// the GPU behind the ABI.
+// -fno-rtti): failures are reported through status().
+//
+// Where the work runs.  Filter builds (Finish, CreateFilter) and batch probes
+// (KeysMayMatch) run on the GPU behind the ABI.  A single-key KeyMayMatch --
+// Table::InternalGet's per-Get call (table/table.cc:357), ~38 ns on the
+// reference's CPU -- is answered on the host from the filter bytes: one GPU
+// round trip per key would cost microseconds.  A GPU call that fails (device
+// error, out of memory, no device) is re-run by the reference's own host
+// loop, so no caller ever receives a 0-byte or partial filter; every such
+// re-run is counted (dlsm_fallback_stats) and the parity tests assert the
+// count stays 0 on their GPU runs.
 #pragma once
 
 #include <cstddef>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -224,6 +234,181 @@ inline bool HasAvx512() { return false; }
 inline size_t DedupStore16(const uint32_t*, size_t, uint32_t, bool, uint8_t*) { return 0; }
 #endif
 
+
+// ---------------------------------------------------------------------------
+// Host forms of the filter arithmetic.  Product code, not the oracle: the
+// single-key probes answer from these, and a build the GPU could not run
+// falls back to them (the reference's own loops, restated).
+// ---------------------------------------------------------------------------
+namespace host {
+
+inline void PutFixed32(char* p, uint32_t v) {  // util/coding.h:130-142 (little-endian)
+  p[0] = static_cast<char>(v);
+  p[1] = static_cast<char>(v >> 8);
+  p[2] = static_cast<char>(v >> 16);
+  p[3] = static_cast<char>(v >> 24);
+}
+inline uint32_t GetFixed32(const char* p) {  // util/coding.h:184-193
+  const unsigned char* u = reinterpret_cast<const unsigned char*>(p);
+  return uint32_t(u[0]) | (uint32_t(u[1]) << 8) | (uint32_t(u[2]) << 16) | (uint32_t(u[3]) << 24);
+}
+
+// LegacyLocalityBloomImpl<false>::AddHash (util/bloom_impl.h:427-443) with
+// 64-byte lines: line h % L, then k bits of that line at h, h + delta, ...
+inline void AddHash(uint32_t h, uint32_t num_lines, int k, char* data) {
+  char* line = data + (static_cast<uint64_t>(h % num_lines) << 6);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int i = 0; i < k; i++) {
+    const uint32_t bitpos = h & 511u;
+    line[bitpos >> 3] = static_cast<char>(line[bitpos >> 3] | (1 << (bitpos & 7)));
+    h += delta;
+  }
+}
+
+// FullFilterBlockBuilder::Finish (table/full_filter_block.cc:93-141) over the
+// hashes h[0, n): CalculateSpace (:61-92) of the consecutive-distinct count,
+// AddHash per kept hash, then the k byte and Fixed32 line count.  dedup drops
+// a hash equal to its predecessor first (AddKey's check, :45-48; the
+// reference's hash_entries_ are already deduplicated).  Writes every byte of
+// the filter, zeros included (the reference ORs into a zeroed slot).  Returns
+// the filter length, or 0 when it does not fit in cap bytes.
+inline uint64_t FullFilterFromHashes(const uint32_t* h, size_t n, int bits_per_key, char* out, size_t cap,
+                                     bool dedup) {
+  uint64_t kept = n;
+  if (dedup) {
+    kept = 0;
+    for (size_t i = 0; i < n; i++) kept += (i == 0 || h[i] != h[i - 1]) ? 1 : 0;
+  }
+  uint32_t L = 0;
+  uint64_t len = 0;
+  dlsm_bloom_full_size(kept, bits_per_key, &L, &len);
+  if (len > cap || !out) return 0;
+  const int k = dlsm_bloom_full_num_probes(bits_per_key);
+  std::memset(out, 0, static_cast<size_t>(L) * 64);
+  if (L)
+    for (size_t i = 0; i < n; i++)
+      if (!dedup || i == 0 || h[i] != h[i - 1]) AddHash(h[i], L, k, out);
+  out[static_cast<size_t>(L) * 64] = static_cast<char>(k);
+  PutFixed32(out + static_cast<size_t>(L) * 64 + 1, L);
+  return len;
+}
+
+// A one-line filter with every bit set ([64 x 0xff][k][Fixed32 1]): the
+// reference reader accepts it (full_filter_block.cc:241-249) and every
+// KeyMayMatch answers true -- never a false negative.  Finish emits it when
+// the slot cannot hold the real filter (the reference only asserts there,
+// :103, and writes past the slot in release builds).  Returns 69, or 0 if
+// cap < 69.
+constexpr size_t kMatchAllLen = 64 + 5;
+inline uint64_t MatchAllFilter(int bits_per_key, char* out, size_t cap) {
+  if (cap < kMatchAllLen || !out) return 0;
+  std::memset(out, 0xff, 64);
+  out[64] = static_cast<char>(dlsm_bloom_full_num_probes(bits_per_key));
+  PutFixed32(out + 65, 1);
+  return kMatchAllLen;
+}
+
+// The parsed metadata of a full filter (FullFilterBlockReader ctor,
+// full_filter_block.cc:186-252, via dlsm_bloom_full_parse: DLSM_E_CORRUPT
+// where the reference exit(1)s or could not probe).
+struct FullFilterMeta {
+  int status = DLSM_E_CORRUPT;
+  int k = 0;
+  uint32_t num_lines = 0;
+  int log2_line = 0;
+};
+inline FullFilterMeta ParseFull(const char* data, size_t len) {
+  FullFilterMeta m;
+  m.status = dlsm_bloom_full_parse(reinterpret_cast<const uint8_t*>(data), len, &m.k, &m.num_lines, &m.log2_line);
+  return m;
+}
+
+// FullFilterBlockReader::KeyMayMatch's probe (full_filter_block.cc:269-284 ->
+// PrepareHashMayMatch / HashMayMatchPrepared, util/bloom_impl.h:445-481) of
+// hash h: line h % L of 2^log2_line bytes, k bits at h, h + delta, ...
+inline bool FullHashMayMatch(const char* data, const FullFilterMeta& m, uint32_t h) {
+  const char* line = data + (static_cast<uint64_t>(h % m.num_lines) << m.log2_line);
+  const uint32_t mask = (1u << (m.log2_line + 3)) - 1u;
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (int i = 0; i < m.k; i++) {
+    const uint32_t bitpos = h & mask;
+    if ((line[bitpos >> 3] & (1 << (bitpos & 7))) == 0) return false;
+    h += delta;
+  }
+  return true;
+}
+
+// BloomFilterPolicy's k (util/bloom.cc:16-21).
+inline int LegacyNumProbes(int bits_per_key) {
+  int k = static_cast<int>(bits_per_key * 0.69);
+  return k < 1 ? 1 : (k > 30 ? 30 : k);
+}
+
+// BloomFilterPolicy::CreateFilter (util/bloom.cc:25-55): the filter of
+// keys[0, n) (each hashed as its first size - suffix_len bytes: the user key
+// of an internal key) into out[0, bytes + 1).  Zeroes the bit array first
+// (the reference ORs into whatever the buffer holds).  Returns bytes + 1.
+inline uint64_t LegacyCreateFilter(const Slice* keys, int n, int bits_per_key, uint32_t suffix_len, char* out) {
+  size_t bits = static_cast<size_t>(n < 0 ? 0 : n) * static_cast<size_t>(bits_per_key);
+  if (bits < 64) bits = 64;
+  const size_t bytes = (bits + 7) / 8;
+  bits = bytes * 8;
+  const int k = LegacyNumProbes(bits_per_key);
+  std::memset(out, 0, bytes);
+  for (int i = 0; i < n; i++) {
+    const size_t len = keys[i].size() >= suffix_len ? keys[i].size() - suffix_len : 0;
+    uint32_t h = BloomHash(keys[i].data(), len);
+    const uint32_t delta = (h >> 17) | (h << 15);
+    for (int j = 0; j < k; j++) {
+      const uint32_t bitpos = static_cast<uint32_t>(h % bits);
+      out[bitpos / 8] = static_cast<char>(out[bitpos / 8] | (1 << (bitpos % 8)));
+      h += delta;
+    }
+  }
+  out[bytes] = static_cast<char>(k);
+  return bytes + 1;
+}
+
+// BloomFilterPolicy::KeyMayMatch (util/bloom.cc:57-81): len < 2 -> false; the
+// stored k read as char -> size_t, > 30 (negative included) -> true.
+inline bool LegacyKeyMayMatch(const char* key, size_t key_len, const char* filter, size_t len) {
+  if (len < 2) return false;
+  const size_t bits = (len - 1) * 8;
+  const size_t k = static_cast<size_t>(static_cast<signed char>(filter[len - 1]));
+  if (k > 30) return true;
+  uint32_t h = BloomHash(key, key_len);
+  const uint32_t delta = (h >> 17) | (h << 15);
+  for (size_t j = 0; j < k; j++) {
+    const uint32_t bitpos = static_cast<uint32_t>(h % bits);
+    if ((filter[bitpos / 8] & (1 << (bitpos % 8))) == 0) return false;
+    h += delta;
+  }
+  return true;
+}
+
+// FilterBlockReader ctor + KeyMayMatch (table/filter_block.cc:114-142) with
+// the legacy policy: the filter of the data block at block_offset, or true
+// ("errors are treated as potential matches").
+inline bool FilterBlockKeyMayMatch(const char* contents, size_t n, uint64_t block_offset, const char* key,
+                                   size_t key_len) {
+  if (n < 5) return true;
+  const unsigned base_lg = static_cast<unsigned>(static_cast<int>(static_cast<signed char>(contents[n - 1])));
+  const uint32_t last_word = GetFixed32(contents + n - 5);
+  if (last_word > n - 5) return true;
+  const char* offset = contents + last_word;
+  const uint64_t num = (n - 5 - last_word) / 4;
+  const uint64_t index = block_offset >> (base_lg & 63u);  // x86 shift count
+  if (index < num) {
+    const uint32_t start = GetFixed32(offset + index * 4);
+    const uint32_t limit = GetFixed32(offset + index * 4 + 4);
+    if (start <= limit && limit <= last_word) return LegacyKeyMayMatch(key, key_len, contents + start, limit - start);
+    if (start == limit) return false;
+  }
+  return true;
+}
+
+}  // namespace host
+
 // Stand-in for the ibv_mr the reference builder borrows: the filter slot.
 // (The reference-signature constructor below takes any type with `addr` and
 // `length` -- ibv_mr itself binds as-is.)
@@ -244,8 +429,12 @@ inline dlsm_ctx* ThreadContext() {
 // (dlsm_host_pool_*): a std::vector<uint32_t, PinnedAllocator<uint32_t>> is
 // the reference's hash_entries_ with its storage in DMA-able memory, so
 // Finish's upload of the hashes runs at the link rate instead of through the
-// runtime's pageable staging.  Like operator new under -fno-exceptions, an
-// allocation failure aborts.
+// runtime's pageable staging.  When the pool cannot page-lock more memory
+// (memlock limit, pinned-memory pressure) the storage comes from malloc
+// instead: the upload is then staged by the runtime, slower but the same
+// bytes.  deallocate tells the two apart by the pool's own answer (it refuses
+// a pointer it did not hand out).  Only an exhausted heap aborts, as operator
+// new does under -fno-exceptions.
 template <class T>
 struct PinnedAllocator {
   using value_type = T;
@@ -255,10 +444,14 @@ struct PinnedAllocator {
   T* allocate(size_t n) {
     void* p = nullptr;
     uint64_t cap = 0;
-    if (dlsm_host_pool_acquire(n * sizeof(T), &p, &cap) != DLSM_OK || !p) std::abort();
+    if (dlsm_host_pool_acquire(n * sizeof(T), &p, &cap) == DLSM_OK && p) return static_cast<T*>(p);
+    p = std::malloc(n * sizeof(T) > 0 ? n * sizeof(T) : 1);
+    if (!p) std::abort();
     return static_cast<T*>(p);
   }
-  void deallocate(T* p, size_t) { dlsm_host_pool_release(p); }
+  void deallocate(T* p, size_t) {
+    if (dlsm_host_pool_release(p) != DLSM_OK) std::free(p);
+  }
   friend bool operator==(const PinnedAllocator&, const PinnedAllocator&) { return true; }
   friend bool operator!=(const PinnedAllocator&, const PinnedAllocator&) { return false; }
 };
@@ -276,7 +469,7 @@ class PinnedBytes {
   PinnedBytes& operator=(const PinnedBytes&) = delete;
   ~PinnedBytes() {
     if (shared_) dlsm_ctx_host_buffer_release(ctx_, this);
-    else if (p_) dlsm_host_pool_release(p_);
+    else if (p_) free_private(p_);
   }
   bool append(const char* d, size_t n) {
     if (size_ + n > cap_ && !grow(size_ + n)) return false;
@@ -311,15 +504,25 @@ class PinnedBytes {
       return true;
     }
     // a private buffer from the library's page-locked pool (builders created
-    // per SSTable recycle them: no page-locking after the first tables)
+    // per SSTable recycle them: no page-locking after the first tables); when
+    // nothing more can be page-locked, from the heap (a slower upload, the
+    // same bytes)
     uint64_t c = 0;
-    const size_t want = need > 2 * cap_ ? need : 2 * cap_;
-    if (dlsm_host_pool_acquire(want > (size_t(1) << 20) ? want : (size_t(1) << 20), &q, &c) != DLSM_OK) return false;
+    size_t want = need > 2 * cap_ ? need : 2 * cap_;
+    if (want < (size_t(1) << 20)) want = size_t(1) << 20;
+    if (dlsm_host_pool_acquire(want, &q, &c) != DLSM_OK || !q) {
+      q = std::malloc(want);
+      if (!q) return false;
+      c = want;
+    }
     if (size_) memcpy(q, p_, size_);
-    if (p_) dlsm_host_pool_release(p_);
+    if (p_) free_private(p_);
     p_ = static_cast<uint8_t*>(q);
     cap_ = c;
     return true;
+  }
+  static void free_private(void* p) {
+    if (dlsm_host_pool_release(p) != DLSM_OK) std::free(p);  // the pool refuses what it did not hand out
   }
   dlsm_ctx* ctx_;
   uint8_t* p_ = nullptr;
@@ -457,8 +660,13 @@ class FullFilterBlockBuilder {
     }
     if (opt_.hash_in_addkey && pend_n_) hash_pending();
     if (stage_status_ != DLSM_OK) {
-      status_ = stage_status_;
-      result.Reset(result.data(), 0);
+      // the keys could not all be staged (host memory exhausted): the
+      // match-everything filter keeps the table readable and exact in the
+      // only sense a Bloom filter must be -- no false negatives
+      device_status_ = status_ = stage_status_;
+      fell_back_ = false;
+      result.Reset(result.data(), host::MatchAllFilter(bits_per_key_, const_cast<char*>(result.data()),
+                                                       output_capacity()));
       clear_keys();
       return;
     }
@@ -496,8 +704,57 @@ class FullFilterBlockBuilder {
     else
       status_ = dlsm_bloom_full_build(ctx_, &job, 1, bits_per_key_, &len);
     if (own_exact) dlsm_ctx_set_option(ctx_, DLSM_OPT_BUILD_EXACT, exact);
+    if (!ctx_ && !opt_.batcher) status_ = DLSM_E_DEVICE;
+    settle(status_, len, [&](std::vector<uint32_t>& h) { staged_hashes(h); });
     clear_keys();
-    result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
+  }
+  // The BloomHash values of the staged keys, in AddKey order (the host
+  // fallback's input): the staged hashes themselves with hash_in_addkey,
+  // else every key hashed.
+  void staged_hashes(std::vector<uint32_t>& h) const {
+    if (opt_.hash_in_addkey) {
+      h.resize(n_);
+      if (n_) std::memcpy(h.data(), keys_.data(), 4 * n_);
+      return;
+    }
+    h.resize(n_);
+    const char* b = reinterpret_cast<const char*>(keys_.data());
+    for (uint64_t i = 0; i < n_; i++)
+      h[i] = uniform_ ? BloomHash(b + i * key_len_, key_len_)
+                      : BloomHash(b + offsets_[i], static_cast<size_t>(offsets_[i + 1] - offsets_[i]));
+  }
+  // The outcome of a Finish whose GPU call returned st (len bytes on
+  // success).  On a device-side failure the reference's own loop builds the
+  // filter on the host from the hashes get_hashes fills (counted:
+  // dlsm_fallback_note); on a slot too small for the filter the
+  // match-everything filter goes in its place (status DLSM_E_CAPACITY).  The
+  // result is never a 0-byte or partial filter unless the buffer cannot hold
+  // even that one (fewer than 69 bytes, or Move_buffer without a size).
+  template <class GetHashes>
+  void settle(int st, uint64_t len, GetHashes get_hashes) {
+    device_status_ = st;
+    fell_back_ = false;
+    char* out = const_cast<char*>(result.data());
+    const size_t cap = output_capacity();
+    if (st == DLSM_OK) {
+      status_ = DLSM_OK;
+      result.Reset(result.data(), len);
+      return;
+    }
+    if (st != DLSM_E_CAPACITY) {
+      dlsm_fallback_note(ctx_);
+      fell_back_ = true;
+      std::vector<uint32_t> h;
+      get_hashes(h);
+      len = host::FullFilterFromHashes(h.data(), h.size(), bits_per_key_, out, cap, true);
+      if (len) {
+        status_ = DLSM_OK;
+        result.Reset(result.data(), len);
+        return;
+      }
+    }
+    status_ = DLSM_E_CAPACITY;
+    result.Reset(result.data(), host::MatchAllFilter(bits_per_key_, out, cap));
   }
 
  public:
@@ -521,7 +778,14 @@ class FullFilterBlockBuilder {
     return moved_cap_;
   }
   int num_probes() const { return num_probes_; }
+  // DLSM_OK: `result` is the exact filter of the table's keys (built on the
+  // GPU, or by the host loop after a GPU failure: fell_back()).
+  // DLSM_E_CAPACITY: the buffer cannot hold it; `result` is the 69-byte
+  // match-everything filter (or empty, below 69 bytes).  device_status(): the
+  // GPU call's own status.
   int status() const { return status_; }
+  int device_status() const { return device_status_; }
+  bool fell_back() const { return fell_back_; }
 
  private:
   // Finish of the reference-signature form: the filter of hash_entries_
@@ -537,9 +801,9 @@ class FullFilterBlockBuilder {
     job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(result.data()));
     job.out_cap = output_capacity();
     uint64_t len = 0;
-    status_ = ctx_ ? dlsm_bloom_full_build_hashed(ctx_, &job, 1, bits_per_key_, &len) : DLSM_E_DEVICE;
+    const int st = ctx_ ? dlsm_bloom_full_build_hashed(ctx_, &job, 1, bits_per_key_, &len) : DLSM_E_DEVICE;
+    settle(st, len, [&](std::vector<uint32_t>& h) { h.assign(hash_entries_.begin(), hash_entries_.end()); });
     hash_entries_.clear();
-    result.Reset(result.data(), status_ == DLSM_OK ? len : 0);
   }
   // BloomHash of the pending keys into the staged hashes, dropping a hash
   // equal to its predecessor (full_filter_block.cc:45-48) branch-free: every
@@ -622,6 +886,8 @@ class FullFilterBlockBuilder {
   uint64_t n_ = 0, dups_ = 0;
   size_t moved_cap_ = 0;
   int status_ = DLSM_OK;        // the last Finish's result
+  int device_status_ = DLSM_OK;  // the last Finish's GPU call
+  bool fell_back_ = false;       // the last Finish's filter came from the host loop
   int stage_status_ = DLSM_OK;  // key staging of the current table
   bool reference_addkey_ = false;
   std::vector<uint32_t, PinnedAllocator<uint32_t>> hash_entries_;  // full_filter_block.h:61
@@ -630,96 +896,207 @@ class FullFilterBlockBuilder {
   Slice result;  // Filter data computed so far
 };
 
+// The filter side of a reader (table/full_filter_block.h:25): a Compute-side
+// reader owns its filter's FilterChunk slot and frees it in its destructor
+// (full_filter_block.cc:285-293).  The reference-signature constructor takes
+// the host's own enum as-is (any enum whose Compute is 0).
+enum FilterSide { Compute, Memory };
+
+namespace detail {
+// Converts to whatever chunk-type enum the manager's
+// Deallocate_Local_RDMA_Slot(void*, Chunk_type) takes: FilterChunk = 5
+// (util/rdma.h:75).
+struct FilterChunkTag {
+  template <class E>
+  operator E() const {  // NOLINT
+    return static_cast<E>(5);
+  }
+};
+// The memory manager a reader holds (std::shared_ptr<RDMA_Manager> in the
+// reference), type-erased; Release frees the filter's slot.
+struct SlotOwner {
+  virtual ~SlotOwner() {}
+  virtual void Release(const char* p) = 0;
+};
+template <class M>
+struct ManagerSlotOwner : SlotOwner {
+  M mgr;
+  explicit ManagerSlotOwner(const M& m) : mgr(m) {}
+  void Release(const char* p) override {
+    if (mgr) (void)mgr->Deallocate_Local_RDMA_Slot(static_cast<void*>(const_cast<char*>(p)), FilterChunkTag{});
+  }
+};
+}  // namespace detail
+
+// table/full_filter_block.h:71-94.  KeyMayMatch (one key: Table::InternalGet,
+// table/table.cc:357) is answered on the host from the filter bytes -- the
+// reference's own arithmetic, no device call.  KeysMayMatch (a batch: a
+// MultiGet over the version's tables) runs on the GPU; the device copy of the
+// filter is made on the first batch, on the calling thread's device, so a
+// reader that never batches holds no device memory.
 class FullFilterBlockReader {
  public:
-  // full_filter_block.cc:186-252: corrupt metadata -> status() ==
-  // DLSM_E_CORRUPT (the reference exit(1)s).
-  FullFilterBlockReader(const Slice& contents, dlsm_ctx* ctx) : filter_content(contents), ctx_(ctx) {
-    status_ = dlsm_bloom_full_parse(reinterpret_cast<const uint8_t*>(contents.data()),
-                                    contents.size(), &num_probes_, &num_lines_, &log2_line_);
-    if (status_ != DLSM_OK) return;
-    const uint8_t* f = reinterpret_cast<const uint8_t*>(contents.data());
-    const uint64_t len = contents.size();
-    status_ = dlsm_filterset_create(ctx_, &f, &len, 1, 0, &fs_);
+  // The reference's signature (full_filter_block.h:76-77):
+  // FullFilterBlockReader(const Slice&, std::shared_ptr<RDMA_Manager>, FilterSide).
+  // `rdma_mg` is any pointer-like manager with Deallocate_Local_RDMA_Slot(void*,
+  // Chunk_type); a Compute-side reader frees the filter's slot through it in
+  // its destructor, as the reference does.  Batches use the calling thread's
+  // context (dlsm_thread_ctx).  Corrupt metadata -> status() DLSM_E_CORRUPT
+  // (the reference exit(1)s) and every probe answers true.
+  template <class M, class Side>
+  FullFilterBlockReader(const Slice& contents, M rdma_mg, Side side)
+      : filter_content(contents), ctx_(nullptr), thread_ctx_(true) {
+    if (static_cast<int>(side) == 0) owner_ = new detail::ManagerSlotOwner<M>(rdma_mg);
+    parse();
+  }
+  // The adapter's form: batches run on `ctx` (nullptr: the calling thread's).
+  FullFilterBlockReader(const Slice& contents, dlsm_ctx* ctx)
+      : filter_content(contents), ctx_(ctx), thread_ctx_(ctx == nullptr) {
+    parse();
   }
   ~FullFilterBlockReader() {
-    if (fs_) dlsm_filterset_destroy(fs_);
+    for (dlsm_filterset* f : fs_)
+      if (f) dlsm_filterset_destroy(f);
+    if (owner_) {
+      owner_->Release(filter_content.data());
+      delete owner_;
+    }
   }
   FullFilterBlockReader(const FullFilterBlockReader&) = delete;
   FullFilterBlockReader& operator=(const FullFilterBlockReader&) = delete;
 
-  bool KeyMayMatch(const Slice& key) {
-    uint8_t m = 0;
-    return KeysMayMatch(&key, 1, &m) == DLSM_OK && m != 0;
+  // full_filter_block.cc:269-284, on the host.
+  bool KeyMayMatch(const Slice& key) const {
+    if (meta_.status != DLSM_OK) return true;  // errors are potential matches
+    return host::FullHashMayMatch(filter_content.data(), meta_, BloomHash(key.data(), key.size()));
   }
-  // Batch form (the GPU's shape): out[i] = 1 if keys[i] may match.
+  // Batch form (the GPU's shape): out[i] = 1 if keys[i] may match.  Runs on
+  // the GPU; if the device cannot take it (no device, device error, out of
+  // memory) the host answers instead (counted: dlsm_fallback_stats), so out
+  // is always filled.  Returns DLSM_OK, or DLSM_E_ARG for a null out / keys.
   int KeysMayMatch(const Slice* keys, size_t n, uint8_t* out) {
-    if (status_ != DLSM_OK) return status_;
-    std::string bytes;
-    std::vector<uint64_t> offs(1, 0);
-    for (size_t i = 0; i < n; i++) {
-      bytes.append(keys[i].data(), keys[i].size());
-      offs.push_back(bytes.size());
+    if (n == 0) return DLSM_OK;
+    if (!keys || !out) return DLSM_E_ARG;
+    dlsm_ctx* ctx = thread_ctx_ ? ThreadContext() : ctx_;
+    int st = meta_.status == DLSM_OK ? DLSM_OK : meta_.status;
+    dlsm_filterset* fs = nullptr;
+    if (st == DLSM_OK) st = ctx ? device_set(ctx, &fs) : DLSM_E_DEVICE;
+    if (st == DLSM_OK) {
+      std::string bytes;
+      std::vector<uint64_t> offs(1, 0);
+      offs.reserve(n + 1);
+      for (size_t i = 0; i < n; i++) {
+        bytes.append(keys[i].data(), keys[i].size());
+        offs.push_back(bytes.size());
+      }
+      if (bytes.empty()) bytes.push_back('\0');
+      dlsm_keyset ks{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0, n};
+      st = dlsm_bloom_full_probe(ctx, fs, &ks, out);
     }
-    dlsm_keyset ks{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0, n};
-    return dlsm_bloom_full_probe(ctx_, fs_, &ks, out);
+    last_device_status_ = st;
+    if (st != DLSM_OK) {
+      if (meta_.status == DLSM_OK) dlsm_fallback_note(ctx);  // a corrupt filter is not a device failure
+      for (size_t i = 0; i < n; i++) out[i] = KeyMayMatch(keys[i]) ? 1 : 0;
+    }
+    return DLSM_OK;
   }
-  int status() const { return status_; }
-  int num_probes() const { return num_probes_; }
-  uint32_t num_lines() const { return num_lines_; }
+  int status() const { return meta_.status; }
+  int num_probes() const { return meta_.k; }
+  uint32_t num_lines() const { return meta_.num_lines; }
+  // The last batch's GPU status (DLSM_OK when the device answered it).
+  int last_device_status() const { return last_device_status_; }
+  // Whether a device copy of the filter exists (made by the first batch).
+  bool device_resident() const {
+    for (dlsm_filterset* f : fs_)
+      if (f) return true;
+    return false;
+  }
 
   Slice filter_content;
 
  private:
+  void parse() { meta_ = host::ParseFull(filter_content.data(), filter_content.size()); }
+  // The filter's device copy on ctx's device, made on first use.  Readers are
+  // shared by reader threads (table_cache.cc:292-299): one copy per device.
+  int device_set(dlsm_ctx* ctx, dlsm_filterset** out) {
+    const int dev = dlsm_ctx_device(ctx);
+    if (dev < 0) return DLSM_E_DEVICE;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (fs_.size() <= static_cast<size_t>(dev)) fs_.resize(static_cast<size_t>(dev) + 1, nullptr);
+    if (!fs_[dev]) {
+      const uint8_t* f = reinterpret_cast<const uint8_t*>(filter_content.data());
+      const uint64_t len = filter_content.size();
+      const int st = dlsm_filterset_create(ctx, &f, &len, 1, 0, &fs_[dev]);
+      if (st != DLSM_OK) {
+        fs_[dev] = nullptr;
+        return st;
+      }
+    }
+    *out = fs_[dev];
+    return DLSM_OK;
+  }
   dlsm_ctx* ctx_;
-  dlsm_filterset* fs_ = nullptr;
-  int num_probes_ = 0;
-  uint32_t num_lines_ = 0;
-  int log2_line_ = 0;
-  int status_ = DLSM_OK;
+  bool thread_ctx_;
+  detail::SlotOwner* owner_ = nullptr;
+  host::FullFilterMeta meta_;
+  std::mutex mu_;
+  std::vector<dlsm_filterset*> fs_;  // by device
+  int last_device_status_ = DLSM_OK;
 };
 
 // The legacy-format policy (util/bloom.cc:14-91) as a FilterPolicy.
 // Name() keeps the reference's format identity string.  suffix_len() = 8
-// makes it hash ExtractUserKey(key) of internal keys on the GPU (the form
-// InternalFilterPolicy wraps it in).
+// makes it hash ExtractUserKey(key) of internal keys (the form
+// InternalFilterPolicy wraps it in).  CreateFilter runs on the GPU (ctx, or
+// the calling thread's context when ctx is nullptr), falling back to the
+// reference's loop on the host if the device cannot take it (counted);
+// KeyMayMatch is one key, answered on the host.
 class BloomFilterPolicy : public FilterPolicy {
  public:
+  // util/bloom.cc:16 -- the reference's signature; builds on the calling
+  // thread's context.
+  explicit BloomFilterPolicy(int bits_per_key) : BloomFilterPolicy(bits_per_key, nullptr) {}
   BloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx, uint32_t suffix_len = 0)
       : bits_per_key_(bits_per_key), ctx_(ctx), suffix_len_(suffix_len) {}
   const char* Name() const override { return "TimberSaw.BuiltinBloomFilter2"; }
 
   // Append a filter summarising keys[0, n) to *dst (util/bloom.cc:25-55).
   void CreateFilter(const Slice* keys, int n, Slice* dst) const override {
+    const int nn = n < 0 ? 0 : n;
     std::string bytes;
     std::vector<uint64_t> offs(1, 0);
-    for (int i = 0; i < n; i++) {
+    offs.reserve(static_cast<size_t>(nn) + 1);
+    for (int i = 0; i < nn; i++) {
       bytes.append(keys[i].data(), keys[i].size());
       offs.push_back(bytes.size());
     }
+    if (bytes.empty()) bytes.push_back('\0');
     uint64_t need = 0;
-    dlsm_bloom_legacy_size(static_cast<uint64_t>(n < 0 ? 0 : n), bits_per_key_, &need);
+    dlsm_bloom_legacy_size(static_cast<uint64_t>(nn), bits_per_key_, &need);
+    char* out = const_cast<char*>(dst->data()) + dst->size();
     dlsm_build_job job;
     job.keys = dlsm_keyset{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, suffix_len_,
-                           static_cast<uint64_t>(n < 0 ? 0 : n)};
-    job.out = reinterpret_cast<uint8_t*>(const_cast<char*>(dst->data())) + dst->size();
+                           static_cast<uint64_t>(nn)};
+    job.out = reinterpret_cast<uint8_t*>(out);
     job.out_cap = need;
     uint64_t len = 0;
-    last_status_ = dlsm_bloom_legacy_build(ctx_, &job, 1, bits_per_key_, &len);
-    if (last_status_ == DLSM_OK) dst->Reset(dst->data(), dst->size() + len);
+    dlsm_ctx* ctx = ctx_ ? ctx_ : ThreadContext();
+    last_status_ = ctx ? dlsm_bloom_legacy_build(ctx, &job, 1, bits_per_key_, &len) : DLSM_E_DEVICE;
+    if (last_status_ != DLSM_OK) {
+      dlsm_fallback_note(ctx);
+      len = host::LegacyCreateFilter(keys, nn, bits_per_key_, suffix_len_, out);
+    }
+    dst->Reset(dst->data(), dst->size() + len);
   }
+  // util/bloom.cc:57-81, on the host.
   bool KeyMayMatch(const Slice& key, const Slice& filter) const override {
-    static const uint8_t z = 0;
-    const uint64_t offs[2] = {0, key.size()};
-    dlsm_keyset ks{key.size() ? reinterpret_cast<const uint8_t*>(key.data()) : &z, offs, 0, suffix_len_, 1};
-    uint8_t r = 0;
-    last_status_ = dlsm_bloom_legacy_probe(ctx_, reinterpret_cast<const uint8_t*>(filter.data()),
-                                           filter.size(), &ks, &r);
-    return last_status_ == DLSM_OK && r != 0;
+    const size_t len = key.size() >= suffix_len_ ? key.size() - suffix_len_ : 0;
+    return host::LegacyKeyMayMatch(key.data(), len, filter.data(), filter.size());
   }
   int bits_per_key() const { return bits_per_key_; }
   dlsm_ctx* ctx() const { return ctx_; }
   uint32_t suffix_len() const { return suffix_len_; }
+  // The last CreateFilter's GPU status (the filter is complete either way).
   int status() const { return last_status_; }
 
  private:
@@ -729,8 +1106,12 @@ class BloomFilterPolicy : public FilterPolicy {
   mutable int last_status_ = DLSM_OK;
 };
 
-// util/bloom.cc:89-91; the caller deletes the result (after every DB using it
-// is closed), as with the reference.
+// util/bloom.cc:89-91 and include/TimberSaw/filter_policy.h:71 -- the
+// reference's signature (db_bench: NewBloomFilterPolicy(FLAGS_bloom_bits),
+// benchmarks/db_bench.cc:638); builds on the calling thread's context.  The
+// caller deletes the result (after every DB using it is closed).
+inline const FilterPolicy* NewBloomFilterPolicy(int bits_per_key) { return new BloomFilterPolicy(bits_per_key); }
+// The same on a given context.
 inline const FilterPolicy* NewBloomFilterPolicy(int bits_per_key, dlsm_ctx* ctx) {
   return new BloomFilterPolicy(bits_per_key, ctx);
 }
@@ -778,7 +1159,7 @@ class InternalFilterPolicy : public FilterPolicy {
 class FilterBlockBuilder {
  public:
   FilterBlockBuilder(FilterSlot* mr, int bits_per_key, dlsm_ctx* ctx)
-      : local_mr_(mr), bits_per_key_(bits_per_key), ctx_(ctx), result(static_cast<char*>(mr->addr), 0) {
+      : result(static_cast<char*>(mr->addr), 0), local_mr_(mr), bits_per_key_(bits_per_key), ctx_(ctx) {
     offsets_.push_back(0);
   }
   FilterBlockBuilder(const FilterBlockBuilder&) = delete;
@@ -796,9 +1177,16 @@ class FilterBlockBuilder {
     dlsm_keyset ks{reinterpret_cast<const uint8_t*>(keys_.data()), offsets_.data(), 0, 0,
                    offsets_.size() - 1};
     uint64_t len = 0;
-    status_ = dlsm_filter_block_build(ctx_, &ks, block_key_end_.data(), block_end_offset_.data(),
-                                      static_cast<int>(block_key_end_.size()), bits_per_key_,
-                                      reinterpret_cast<uint8_t*>(local_mr_->addr), local_mr_->length, &len);
+    dlsm_ctx* ctx = ctx_ ? ctx_ : ThreadContext();
+    status_ = ctx ? dlsm_filter_block_build(ctx, &ks, block_key_end_.data(), block_end_offset_.data(),
+                                            static_cast<int>(block_key_end_.size()), bits_per_key_,
+                                            reinterpret_cast<uint8_t*>(local_mr_->addr), local_mr_->length, &len)
+                  : DLSM_E_DEVICE;
+    if (status_ != DLSM_OK && status_ != DLSM_E_CAPACITY) {
+      dlsm_fallback_note(ctx);
+      len = host_finish();
+      status_ = len ? DLSM_OK : DLSM_E_CAPACITY;
+    }
     result.Reset(static_cast<char*>(local_mr_->addr), status_ == DLSM_OK ? len : 0);
     return result;
   }
@@ -808,6 +1196,51 @@ class FilterBlockBuilder {
   Slice result;
 
  private:
+  // filter_block.cc:32-113 on the host (the GPU call failed): replays the
+  // recorded StartBlock / AddKey sequence -- a filter per 2 KiB of block
+  // offsets (GenerateFilter at each StartBlock that crosses into a later
+  // 2 KiB range, and at Finish for keys still pending), then the Fixed32
+  // offsets, the array offset and kFilterBaseLg.  Returns the block's length,
+  // 0 if the slot is too small.
+  uint64_t host_finish() {
+    const size_t n_keys = offsets_.size() - 1;
+    uint64_t need = 5;
+    size_t done = 0;  // keys already in a filter
+    std::vector<uint32_t> foffs;
+    std::vector<Slice> tmp;
+    char* out = static_cast<char*>(local_mr_->addr);
+    const size_t cap = local_mr_->length;
+    auto generate = [&](size_t upto) -> bool {
+      foffs.push_back(static_cast<uint32_t>(need - 5));
+      if (upto == done) return true;
+      uint64_t sz = 0;
+      dlsm_bloom_legacy_size(upto - done, bits_per_key_, &sz);
+      if (need + sz + 4 * (foffs.size() + 1) > cap) return false;
+      tmp.clear();
+      for (size_t i = done; i < upto; i++)
+        tmp.emplace_back(keys_.data() + offsets_[i], static_cast<size_t>(offsets_[i + 1] - offsets_[i]));
+      host::LegacyCreateFilter(tmp.data(), static_cast<int>(tmp.size()), bits_per_key_, 0, out + need - 5);
+      need += sz;
+      done = upto;
+      return true;
+    };
+    for (size_t b = 0; b < block_key_end_.size(); b++) {
+      const uint64_t index = block_end_offset_[b] >> 11;  // kFilterBaseLg
+      while (index > foffs.size())
+        if (!generate(static_cast<size_t>(block_key_end_[b]))) return 0;
+    }
+    if (done < n_keys && !generate(n_keys)) return 0;
+    const uint64_t array_offset = need - 5;
+    if (array_offset + 4 * foffs.size() + 5 > cap) return 0;
+    char* p = out + array_offset;
+    for (uint32_t f : foffs) {
+      host::PutFixed32(p, f);
+      p += 4;
+    }
+    host::PutFixed32(p, static_cast<uint32_t>(array_offset));
+    p[4] = 11;
+    return array_offset + 4 * foffs.size() + 5;
+  }
   FilterSlot* local_mr_;
   int bits_per_key_;
   dlsm_ctx* ctx_;
@@ -817,14 +1250,29 @@ class FilterBlockBuilder {
   int status_ = DLSM_OK;
 };
 
+// table/filter_block.h:70-85.  KeyMayMatch (one key) on the host from the
+// block's bytes; KeysMayMatch (a batch) on the GPU (ctx, or the calling
+// thread's context when ctx is nullptr).
 class FilterBlockReader {
  public:
   FilterBlockReader(const Slice& contents, dlsm_ctx* ctx) : contents_(contents), ctx_(ctx) {}
-  bool KeyMayMatch(uint64_t block_offset, const Slice& key) {
-    uint8_t m = 0;
-    return KeysMayMatch(&block_offset, &key, 1, &m) == DLSM_OK && m != 0;
+  // filter_block.cc:127-142, on the host.
+  bool KeyMayMatch(uint64_t block_offset, const Slice& key) const {
+    return host::FilterBlockKeyMayMatch(contents_.data(), contents_.size(), block_offset, key.data(), key.size());
   }
   int KeysMayMatch(const uint64_t* block_offsets, const Slice* keys, size_t n, uint8_t* out) {
+    dlsm_ctx* ctx = ctx_ ? ctx_ : ThreadContext();
+    const int st = ctx ? device_batch(ctx, block_offsets, keys, n, out) : DLSM_E_DEVICE;
+    if (st != DLSM_OK && n && keys && out && block_offsets) {  // the host answers instead (counted)
+      dlsm_fallback_note(ctx);
+      for (size_t i = 0; i < n; i++) out[i] = KeyMayMatch(block_offsets[i], keys[i]) ? 1 : 0;
+      return DLSM_OK;
+    }
+    return st;
+  }
+
+ private:
+  int device_batch(dlsm_ctx* ctx, const uint64_t* block_offsets, const Slice* keys, size_t n, uint8_t* out) {
     std::string bytes;
     std::vector<uint64_t> offs(1, 0);
     for (size_t i = 0; i < n; i++) {
@@ -833,11 +1281,9 @@ class FilterBlockReader {
     }
     if (bytes.empty()) bytes.push_back('\0');
     dlsm_keyset ks{reinterpret_cast<const uint8_t*>(bytes.data()), offs.data(), 0, 0, n};
-    return dlsm_filter_block_probe(ctx_, reinterpret_cast<const uint8_t*>(contents_.data()),
+    return dlsm_filter_block_probe(ctx, reinterpret_cast<const uint8_t*>(contents_.data()),
                                    contents_.size(), &ks, block_offsets, out);
   }
-
- private:
   Slice contents_;
   dlsm_ctx* ctx_;
 };

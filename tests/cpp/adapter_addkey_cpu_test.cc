@@ -49,6 +49,14 @@ int dlsm_bloom_full_build_hashed(dlsm_ctx*, const dlsm_build_job* j, int n_jobs,
 int dlsm_batcher_full_build(dlsm_batcher*, const dlsm_build_job*, int, uint64_t*) { return DLSM_E_ARG; }
 int dlsm_batcher_full_build_hashed(dlsm_batcher*, const dlsm_build_job*, int, uint64_t*) { return DLSM_E_ARG; }
 int dlsm_batcher_submit(dlsm_batcher*, const dlsm_build_job*, int, int, uint64_t*) { return DLSM_E_ARG; }
+int dlsm_bloom_full_size(uint64_t n, int bpk, uint32_t* L, uint64_t* nbytes) {  // the host fallback's sizing
+  uint32_t lines = n ? (static_cast<uint32_t>(n * bpk) + 511) / 512 : 0;
+  if (lines && lines % 2 == 0) lines++;
+  if (L) *L = lines;
+  if (nbytes) *nbytes = uint64_t(lines) * 64 + 5;
+  return DLSM_OK;
+}
+void dlsm_fallback_note(dlsm_ctx*) {}
 static int g_thread_ctx_token;
 int dlsm_thread_ctx(dlsm_ctx** out) {
   *out = reinterpret_cast<dlsm_ctx*>(&g_thread_ctx_token);  // only passed to the stubs

@@ -160,7 +160,7 @@ int main() {
     bad[65] = 1;  // k byte 0
     dlsm_adapter::FullFilterBlockReader r(Slice(bad, sizeof(bad)), ctx);
     CHECK(r.status() == DLSM_E_CORRUPT);
-    CHECK(!r.KeyMayMatch(Slice("x", 1)));
+    CHECK(r.KeyMayMatch(Slice("x", 1)));  // errors are potential matches
   }
   // ---- BloomFilterPolicy (legacy format) ----
   {
@@ -442,7 +442,10 @@ int main() {
     b.Move_buffer(other.data(), other.size());  // 4 KiB < the 5,000-key filter's 6,341 bytes
     add(10000);
     b.Finish();
-    CHECK(b.status() == DLSM_E_CAPACITY && b.result.size() == 0);
+    // too small: the 69-byte match-everything filter, never a 0-byte one
+    CHECK(b.status() == DLSM_E_CAPACITY && b.result.size() == 69 && !b.fell_back());
+    for (int i = 0; i < 64; i++) CHECK(static_cast<uint8_t>(other[i]) == 0xff);
+    CHECK(other[64] == 6 && other[65] == 1 && other[66] == 0 && other[67] == 0 && other[68] == 0);
     b.Move_buffer(other.data(), other.size());
     add(2000);  // 1,000 distinct keys: 1,349 bytes
     b.Finish();
@@ -451,6 +454,9 @@ int main() {
     CHECK(dlsm_ctx_get_option(ctx, DLSM_OPT_BUILD_EXACT, &ex) == DLSM_OK && ex == 2);
     CHECK(dlsm_ctx_set_option(ctx, DLSM_OPT_BUILD_EXACT, 0) == DLSM_OK);
   }
+  // no call of this test fell back to the host: the GPU served all of them
+  uint64_t fb_ctx = 1, fb_all = 1;
+  CHECK(dlsm_fallback_stats(ctx, &fb_ctx, &fb_all) == DLSM_OK && fb_ctx == 0 && fb_all == 0);
   dlsm_ctx_destroy(ctx);
   std::printf("OK adapter\n");
   return 0;

@@ -86,6 +86,34 @@ def test_adapter_addkey_hashing_on_cpu(tmp_path):
     assert out.returncode == 0 and "OK adapter addkey cpu" in out.stdout, out.stdout + out.stderr
 
 
+def test_adapter_fallback_without_device(tmp_path):
+    """With no device visible (this CPU suite) the reference-signature builder,
+    reader, policy and legacy filter block still produce the oracle's bytes
+    and answers: every GPU call fails and the host loops (product code in the
+    adapter) answer instead, each counted by dlsm_fallback_stats.  On a box
+    with a GPU the same program runs its GPU form (test below)."""
+    exe = _compile(tmp_path, "adapter_fallback_test")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "OK adapter fallback" in out.stdout, out.stdout + out.stderr
+
+
+@pytest.mark.gpu
+def test_adapter_fallback_and_reference_signatures_on_gpu(tmp_path):
+    """The drop-in's failure path and reference signatures on the GPU:
+    FullFilterBlockBuilder(ibv_mr*, int) with injected DLSM_E_DEVICE /
+    DLSM_E_NOMEM at 0, 1, 7 and 153,846 keys emits the oracle's filter (host
+    re-run, counted), never a 0-byte one; FullFilterBlockReader(Slice,
+    shared_ptr<Manager>, FilterSide) and NewBloomFilterPolicy(int) answer
+    single keys on the host with no device copy until the first batch, batches
+    on the GPU; single-key latency is reported in ns."""
+    exe = _compile(tmp_path, "adapter_fallback_test")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "OK adapter fallback" in out.stdout, out.stdout + out.stderr
+    rec = json.loads(out.stdout.splitlines()[0])
+    assert rec["device"] is True
+    print(json.dumps(rec))
+
+
 @pytest.mark.gpu
 def test_adapter_on_gpu(tmp_path):
     exe = _compile(tmp_path, "adapter_test")

@@ -91,6 +91,24 @@ def test_legacy_shapes_vs_oracle(gpu, orc):
             assert g == w, (bpk, n)
 
 
+def test_legacy_forced_sliced_path_falls_back_to_direct(gpu, orc):
+    """Path 2 (sliced forced) with a batch the tiled kernels cannot take --
+    bits_per_key 14 (k = 9 > 8) -- builds on the direct kernel with the same
+    bytes instead of failing: a context set to path 2 for its full
+    filters keeps building legacy ones."""
+    import dlsm_amd
+
+    sizes = [1, 7, 4097, 200_000]
+    tabs = [orc.dbbench_keys(3 + s, 8, n) for s, n in enumerate(sizes)]
+    gpu.set_path(2)
+    try:
+        for bpk in (10, 14, 20):
+            got = gpu.legacy_build([dlsm_amd.Keys(t, n, 20) for t, n in zip(tabs, sizes)], bpk)
+            assert got == [orc.legacy_build(t, n, bpk=bpk) for t, n in zip(tabs, sizes)], bpk
+    finally:
+        gpu.set_path(0)
+
+
 def test_legacy_varlen_and_internal_keys(gpu, orc):
     """Variable-length keys (offsets, generic loader) and 28-byte internal
     keys (suffix 8: ExtractUserKey, K28 loader) on the tiled path."""

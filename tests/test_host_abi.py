@@ -143,3 +143,17 @@ def test_cu_subset_is_balanced_under_both_numberings():
         assert len(s) == 8 * per and len(set(s)) == len(s)
         assert all(sum(1 for i in s if i // 32 == x) == per for x in range(8))
         assert all(sum(1 for i in s if i % 8 == x) == per for x in range(8))
+
+
+def test_keys_guard_checks_data_against_host_offsets():
+    """Variable-length Keys with host offsets: a data buffer shorter than
+    offsets[n] is refused before any pointer reaches the library."""
+    import dlsm_amd
+
+    offs = np.array([0, 5, 12], dtype=np.uint64)
+    ok = dlsm_amd.Keys(np.zeros(12, dtype=np.uint8), 2, 0, offs)
+    ok.c()
+    with pytest.raises(ValueError):
+        dlsm_amd.Keys(np.zeros(11, dtype=np.uint8), 2, 0, offs).c()
+    with pytest.raises(ValueError):
+        dlsm_amd.Keys(np.zeros(12, dtype=np.uint8), 2, 0, offs[:2]).c()
