@@ -349,6 +349,10 @@ def main():
         "value": round(value, 2),
         "unit": "Mkeys/s",
         "n_gpus": world,
+        # ranks sharing a GPU (DLSM_BENCH_BACKEND=gloo on a smaller box) rehearse
+        # the N-GPU path: such a line is not an N-GPU measurement
+        "rehearsed": world > torch.cuda.device_count(),
+        "physical_devices": min(world, torch.cuda.device_count()),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -549,6 +553,10 @@ def threads_line(args, n_gpu, devices, workers, per_gpu, elapsed, T, N, Q, F, bp
         "value": round(value, 2),
         "unit": "Mkeys/s",
         "n_gpus": n_gpu,
+        # --rehearse maps the N logical devices onto fewer physical ones: such a
+        # line is not an N-GPU measurement
+        "rehearsed": bool(args.rehearse),
+        "physical_devices": len(set(devices)),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),

@@ -109,6 +109,8 @@ struct dlsm_ctx {
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
   int fault = 0;              // DLSM_OPT_FAULT_INJECT: > 0 -> builds / probes return -fault
+  uint64_t vslice_bytes = 0;  // DLSM_OPT_VERSION_SLICE_BYTES (0: default)
+  uint32_t vpass_slices = kVMaxSlices;  // DLSM_OPT_VERSION_PASS_SLICES
   std::atomic<uint64_t> fallbacks{0};  // dlsm_fallback_note: host re-runs of this context's failed calls
   // build workspace
   DevBuf<uint32_t> entries;
@@ -132,7 +134,11 @@ struct dlsm_ctx {
   DevBuf<uint16_t> lentries;  // u16 bit positions per tile bucket
   DevBuf<uint16_t> ltab;      // chunk-major tile-bucket offsets
   // probe workspace
-  DevBuf<uint32_t> hashes;  // grouped probe: one BloomHash per lookup
+  DevBuf<uint32_t> hashes;  // grouped probe / sliced version probe: one BloomHash per lookup
+  DevBuf<uint32_t> vgl;     // sliced version probe: per sliced level, each lookup's global line
+  DevBuf<uint8_t> vabyte;   // sliced version probe: per lookup, the sliced levels' answer bits
+  DevBuf<uint32_t> vplan;   // sliced version probe: per-slice unit counters | slice-pass plan
+  uint64_t vplan_zeroed = 0;  // vplan's allocation generation whose counters were zeroed
   DevBuf<uint16_t> pos;
   DevBuf<uint8_t> smask;
   // host-API staging
@@ -632,6 +638,9 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->ltab.release();
   ctx->pos.release();
   ctx->hashes.release();
+  ctx->vgl.release();
+  ctx->vabyte.release();
+  ctx->vplan.release();
   ctx->smask.release();
   ctx->sel.release();
   ctx->st_keys.release();
@@ -681,6 +690,8 @@ void ctx_pool_put(dlsm_ctx* c) {
   c->pstream = nullptr;
   c->pcus = 0;
   c->fault = 0;
+  c->vslice_bytes = 0;
+  c->vpass_slices = kVMaxSlices;
   {
     std::lock_guard<std::mutex> lo(g_opts_m);
     auto it = g_opts.find(c);
@@ -782,6 +793,13 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value > static_cast<uint64_t>(-DLSM_E_BUSY)) return DLSM_E_ARG;
       ctx->fault = static_cast<int>(value);
       return DLSM_OK;
+    case DLSM_OPT_VERSION_SLICE_BYTES:
+      ctx->vslice_bytes = value;
+      return DLSM_OK;
+    case DLSM_OPT_VERSION_PASS_SLICES:
+      if (value < 1 || value > kVMaxSlices) return DLSM_E_ARG;
+      ctx->vpass_slices = static_cast<uint32_t>(value);
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -798,6 +816,8 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_BUILD_EXACT: *value = static_cast<uint64_t>(ctx->build_exact); return DLSM_OK;
     case DLSM_OPT_PROBE_ROUND_SERIAL: *value = ctx->probe_serial ? 1u : 0u; return DLSM_OK;
     case DLSM_OPT_FAULT_INJECT: *value = static_cast<uint64_t>(ctx->fault); return DLSM_OK;
+    case DLSM_OPT_VERSION_SLICE_BYTES: *value = ctx->vslice_bytes; return DLSM_OK;
+    case DLSM_OPT_VERSION_PASS_SLICES: *value = ctx->vpass_slices; return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -834,6 +854,7 @@ int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_byte
   add(ctx->entries); add(ctx->tab); add(ctx->jobs); add(ctx->starts); add(ctx->dchunk);
   add(ctx->jobL); add(ctx->ljobs); add(ctx->lstarts); add(ctx->ltjobs); add(ctx->ltstarts);
   add(ctx->lentries); add(ctx->ltab); add(ctx->pos); add(ctx->smask); add(ctx->hashes);
+  add(ctx->vgl); add(ctx->vabyte); add(ctx->vplan);
   add(ctx->st_keys); add(ctx->st_offs); add(ctx->st_out); add(ctx->st_len); add(ctx->st_filter);
   add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_outp); add(ctx->crc_cap);
   add(ctx->crc_val); add(ctx->sel);
@@ -2033,12 +2054,40 @@ int dlsm_filter_block_probe(dlsm_ctx* ctx, const uint8_t* block, uint64_t len, c
 // ---------------------------------------------------------------------------
 static_assert(DLSM_NUM_LEVELS == kNumLevels, "config::kNumLevels");
 
+// A level probed by the sliced version probe: its filters' lines back to
+// back in one image (`image`, `lines` lines of 64 B, one probe count `k`).
+struct VersionLevel {
+  int level = 0;
+  int k = 0;
+  uint32_t lines = 0;
+  const uint8_t* image = nullptr;
+};
+
 struct dlsm_version {
   int device = 0;
   VersionDev v{};
   int n_files = 0;
-  uint8_t* mem = nullptr;  // one allocation: files | key blob | filters
+  uint8_t* mem = nullptr;  // one allocation: files | key blob | filters (sliced levels: their images)
+  std::vector<VersionLevel> sliced;
 };
+
+namespace {
+// A level >= 1 goes to the sliced probe when its filters hold more than this
+// many bytes and every filter of the level has 64-byte lines and one probe
+// count.  Default 256 MiB, the Infinity Cache: below it the direct probe's
+// line reads (four lanes per line, tasks queued per wave) are served on-die
+// and beat a partition / slice / unpermute round per level -- the db_bench
+// version (139.5 MB of filters) takes 4.0 ms direct against 5.4 ms with its
+// two big levels sliced (profiles/r05_version_probe.txt).
+// ($DLSM_VERSION_SLICE_MIN_BYTES overrides; 0 disables the sliced probe.)
+uint64_t version_slice_min_bytes() {
+  static const uint64_t v = [] {
+    const char* e = getenv("DLSM_VERSION_SLICE_MIN_BYTES");
+    return e ? strtoull(e, nullptr, 10) : (uint64_t(256) << 20);
+  }();
+  return v;
+}
+}  // namespace
 
 int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_files,
                         int filters_are_device, dlsm_version** out) {
@@ -2102,7 +2151,46 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
   }
   const uint64_t pre_bytes = (sizeof(ulonglong2) * pre.size() + 255) & ~uint64_t(255);
   const uint64_t keys_bytes = (keys.size() + 255) & ~uint64_t(255);
-  uint64_t total = files_bytes + pre_bytes + keys_bytes;
+  // The interval index (VIntervalDev): the distinct bound prefixes in order,
+  // and per open interval between two of them the level-0 files that hold
+  // it and each level's FindFile pick.  For a lookup prefix strictly between
+  // bnd[j-1] and bnd[j]: a bound with prefix index < j sorts below the lookup,
+  // one with index >= j above it.
+  auto pre_lt = [](const ulonglong2& a, const ulonglong2& b) { return a.x < b.x || (a.x == b.x && a.y < b.y); };
+  std::vector<ulonglong2> bnd(pre);
+  std::sort(bnd.begin(), bnd.end(), pre_lt);
+  bnd.erase(std::unique(bnd.begin(), bnd.end(),
+                        [](const ulonglong2& a, const ulonglong2& b) { return a.x == b.x && a.y == b.y; }),
+            bnd.end());
+  auto bidx = [&](const ulonglong2& p) {
+    return static_cast<uint32_t>(std::lower_bound(bnd.begin(), bnd.end(), p, pre_lt) - bnd.begin());
+  };
+  std::vector<uint32_t> is(n_files), il(n_files);
+  for (int j = 0; j < n_files; j++) {
+    is[j] = bidx(pre[j]);
+    il[j] = bidx(pre[n_files + j]);
+  }
+  const uint32_t n_bnd = static_cast<uint32_t>(bnd.size());
+  std::vector<VIntervalDev> ivl(n_bnd + 1);
+  for (uint32_t j = 0; j <= n_bnd; j++) {
+    VIntervalDev& r = ivl[j];
+    r.l0mask = 0;
+    r.reserved = 0;
+    for (int f = 0; f < n_l0; f++)  // smallest <= lookup <= largest
+      if (is[f] < j && il[f] >= j) r.l0mask |= 1ull << f;
+    for (int lv = 1; lv < kNumLevels; lv++) {
+      r.pick[lv - 1] = 0xffffffffu;
+      if (!count[lv]) continue;
+      // FindFile (version_set.cc:95-118): files [0, count-1) whose largest
+      // sorts below the lookup come first; right starts at count-1
+      uint32_t right = 0;
+      while (right < count[lv] - 1 && il[begin[lv] + right] < j) right++;
+      if (is[begin[lv] + right] < j) r.pick[lv - 1] = begin[lv] + right;
+    }
+  }
+  const uint64_t bnd_bytes = (sizeof(ulonglong2) * std::max<size_t>(1, bnd.size()) + 255) & ~uint64_t(255);
+  const uint64_t ivl_bytes = (sizeof(VIntervalDev) * ivl.size() + 255) & ~uint64_t(255);
+  uint64_t total = files_bytes + pre_bytes + keys_bytes + bnd_bytes + ivl_bytes;
   for (int j = 0; j < n_files; j++) {
     const dlsm_version_file& F = files[order[j]];
     if (!F.filter) continue;
@@ -2121,7 +2209,52 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
     h[j].f.magic = fastmod_magic(L);
     h[j].f.k = k;
     h[j].f.lg = lg;
+  }
+  // Levels for the sliced probe; their filters' lines are laid out back to
+  // back (line0 per file), the other filters one by one, 256-byte aligned.
+  std::vector<VersionLevel> sliced;
+  int32_t lvl_sliced[kNumLevels];
+  std::vector<uint64_t> copy_len(n_files, 0);
+  for (int lv = 0; lv < kNumLevels; lv++) lvl_sliced[lv] = -1;
+  const uint64_t min_bytes = ctx->vslice_bytes == 0 ? version_slice_min_bytes()
+                             : (ctx->vslice_bytes == UINT64_MAX ? 0 : ctx->vslice_bytes);
+  for (int lv = 1; lv < kNumLevels && min_bytes; lv++) {
+    uint64_t lines = 0;
+    int k = 0;
+    bool ok = true;
+    for (uint32_t j = begin[lv]; j < begin[lv] + count[lv]; j++) {
+      if (!files[order[j]].filter) continue;
+      ok = ok && h[j].f.lg == 6 && (k == 0 || h[j].f.k == k);
+      k = h[j].f.k;
+      lines += h[j].f.L;
+    }
+    if (!ok || lines * 64 <= min_bytes || lines >= kVNoLine) continue;
+    lvl_sliced[lv] = static_cast<int32_t>(sliced.size());
+    VersionLevel vl;
+    vl.level = lv;
+    vl.k = k;
+    vl.lines = static_cast<uint32_t>(lines);
+    sliced.push_back(vl);
+  }
+  std::vector<uint64_t> image_off(sliced.size(), 0);
+  for (size_t q = 0; q < sliced.size(); q++) {
+    const int lv = sliced[q].level;
+    image_off[q] = total;
+    uint32_t line0 = 0;
+    for (uint32_t j = begin[lv]; j < begin[lv] + count[lv]; j++) {
+      if (!files[order[j]].filter) continue;
+      h[j].line0 = line0;
+      foff[j] = total + static_cast<uint64_t>(line0) * 64;
+      copy_len[j] = static_cast<uint64_t>(h[j].f.L) * 64;  // the lines; the trailer was parsed above
+      line0 += h[j].f.L;
+    }
+    total += (static_cast<uint64_t>(sliced[q].lines) * 64 + 255) & ~uint64_t(255);
+  }
+  for (int j = 0; j < n_files; j++) {
+    const dlsm_version_file& F = files[order[j]];
+    if (!F.filter || copy_len[j]) continue;
     foff[j] = total;
+    copy_len[j] = F.filter_len;
     total += (F.filter_len + 255) & ~uint64_t(255);
   }
   dlsm_version* ver = new (std::nothrow) dlsm_version();
@@ -2133,9 +2266,11 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
     const dlsm_version_file& F = files[order[j]];
     if (!F.filter) continue;
     h[j].f.data = ver->mem + foff[j];
-    e = hipMemcpyAsync(ver->mem + foff[j], F.filter, F.filter_len,
+    e = hipMemcpyAsync(ver->mem + foff[j], F.filter, copy_len[j],
                        filters_are_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s);
   }
+  for (size_t q = 0; q < sliced.size(); q++) sliced[q].image = ver->mem + image_off[q];
+  ver->sliced = sliced;
   if (e == hipSuccess && n_files)
     e = hipMemcpyAsync(ver->mem, h.data(), sizeof(VFileDev) * n_files, hipMemcpyHostToDevice, s);
   if (e == hipSuccess && n_files)
@@ -2143,6 +2278,12 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
                        hipMemcpyHostToDevice, s);
   if (e == hipSuccess && !keys.empty())
     e = hipMemcpyAsync(ver->mem + files_bytes + pre_bytes, keys.data(), keys.size(), hipMemcpyHostToDevice, s);
+  const uint64_t bnd_off = files_bytes + pre_bytes + keys_bytes;
+  if (e == hipSuccess && !bnd.empty())
+    e = hipMemcpyAsync(ver->mem + bnd_off, bnd.data(), sizeof(ulonglong2) * bnd.size(), hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ver->mem + bnd_off + bnd_bytes, ivl.data(), sizeof(VIntervalDev) * ivl.size(),
+                       hipMemcpyHostToDevice, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);  // pageable sources: finish before returning
   if (e != hipSuccess) {
     dlsm_version_destroy(ver);
@@ -2152,10 +2293,25 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
   ver->v.pre_small = reinterpret_cast<const ulonglong2*>(ver->mem + files_bytes);
   ver->v.pre_large = ver->v.pre_small + n_files;
   ver->v.keyblob = ver->mem + files_bytes + pre_bytes;
+  ver->v.bnd = reinterpret_cast<const ulonglong2*>(ver->mem + bnd_off);
+  ver->v.ivl = reinterpret_cast<const VIntervalDev*>(ver->mem + bnd_off + bnd_bytes);
+  ver->v.n_bnd = n_bnd;
+  ver->v.k_all = 0;
+  {
+    int kc = 0;
+    bool same = true;
+    for (int j = 0; j < n_files; j++) {
+      if (!files[order[j]].filter) continue;
+      same = same && (kc == 0 || h[j].f.k == kc);
+      kc = h[j].f.k;
+    }
+    ver->v.k_all = same ? kc : 0;
+  }
   ver->v.n_l0 = static_cast<uint32_t>(n_l0);
   for (int lv = 0; lv < kNumLevels; lv++) {
     ver->v.lvl_begin[lv] = begin[lv];
     ver->v.lvl_count[lv] = count[lv];
+    ver->v.lvl_sliced[lv] = lvl_sliced[lv];
   }
   *out = ver;
   return DLSM_OK;
@@ -2184,8 +2340,65 @@ int dlsm_version_probe_dev(dlsm_ctx* ctx, const dlsm_version* v, const dlsm_keys
   DLSM_CHECK(validate_keyset(*keys));
   if (keys->n == 0) return DLSM_OK;
   if (!slot_mask_dev) return DLSM_E_ARG;
+  if (ctx->fault) return -ctx->fault;
   DeviceGuard g(ctx->device);
-  DLSM_TRY(launch_version_probe(v->v, to_desc(*keys), snapshot, slot_mask_dev, level_file_dev, ctx->stream));
+  hipStream_t s = ctx->stream;
+  const KeyDesc kd = to_desc(*keys);
+  if (v->sliced.empty() || ctx->path == 1) {
+    // every level probed directly: one thread per lookup, filter lines read
+    // where they lie (the L2-resident shape)
+    VersionDev vd = v->v;
+    for (int lv = 0; lv < kNumLevels; lv++) vd.lvl_sliced[lv] = -1;
+    DLSM_TRY(launch_version_probe(vd, kd, snapshot, slot_mask_dev, level_file_dev, s));
+    return DLSM_OK;
+  }
+  // Sliced: a route pass (the direct levels answered, each sliced level's
+  // global line per lookup), then per sliced level and group of up to
+  // kVMaxSlices slices a partition / LDS slice / unpermute round.
+  const uint64_t n = keys->n;
+  const int J = static_cast<int>(v->sliced.size());
+  const uint32_t nC = ceil_div_u32(n, kVChunk);
+  const uint64_t span = static_cast<uint64_t>(ctx->vpass_slices) << kVSliceLg;
+  struct Pass {
+    int j;
+    uint32_t g0, S, L;
+  };
+  std::vector<Pass> passes;
+  uint32_t Smax = 1;
+  for (int j = 0; j < J; j++)
+    for (uint64_t g0 = 0; g0 < v->sliced[j].lines; g0 += span) {
+      const uint32_t L = static_cast<uint32_t>(std::min<uint64_t>(v->sliced[j].lines - g0, span));
+      const uint32_t S = ceil_div_u32(L, 1u << kVSliceLg);
+      passes.push_back(Pass{j, static_cast<uint32_t>(g0), S, L});
+      Smax = std::max(Smax, S);
+    }
+  uint64_t slots = 0;
+  for (int j = 0; j < J; j++) slots |= static_cast<uint64_t>(v->v.n_l0 + v->sliced[j].level - 1) << (8 * j);
+  DLSM_CHECK(ctx->hashes.ensure(n));
+  DLSM_CHECK(ctx->vgl.ensure(static_cast<uint64_t>(J) * n));
+  DLSM_CHECK(ctx->entries.ensure(static_cast<uint64_t>(nC) * kVRegion));
+  DLSM_CHECK(ctx->smask.ensure(static_cast<uint64_t>(nC) * kVRegion));
+  DLSM_CHECK(ctx->pos.ensure(static_cast<uint64_t>(nC) * kVChunk));
+  DLSM_CHECK(ctx->tab.ensure(static_cast<uint64_t>(nC) * (Smax + 1)));
+  if (passes.size() > 1) DLSM_CHECK(ctx->vabyte.ensure(n));
+  DLSM_CHECK(ctx->vplan.ensure(2 * (kVMaxSlices + 1)));
+  uint32_t* gcnt = ctx->vplan.p;
+  uint32_t* plan = ctx->vplan.p + kVMaxSlices + 1;
+  if (ctx->vplan_zeroed != ctx->vplan.gen) {  // the plan kernel re-zeroes the counters after every pass
+    DLSM_TRY(hipMemsetAsync(gcnt, 0, sizeof(uint32_t) * (kVMaxSlices + 1), s));
+    ctx->vplan_zeroed = ctx->vplan.gen;
+  }
+  DLSM_TRY(launch_version_route(v->v, kd, snapshot, slot_mask_dev, level_file_dev, ctx->hashes.p, ctx->vgl.p, s));
+  for (size_t p = 0; p < passes.size(); p++) {
+    const Pass& P = passes[p];
+    const VersionLevel& VL = v->sliced[P.j];
+    DLSM_TRY(launch_version_partition(ctx->hashes.p, ctx->vgl.p + static_cast<uint64_t>(P.j) * n, n, P.g0, P.S,
+                                      ctx->entries.p, ctx->pos.p, ctx->tab.p, gcnt, plan, s));
+    DLSM_TRY(launch_version_slices(VL.image + static_cast<uint64_t>(P.g0) * 64, P.L, VL.k, P.S, nC,
+                                   ctx->entries.p, ctx->tab.p, ctx->smask.p, plan, s));
+    DLSM_TRY(launch_version_unpermute(n, ctx->pos.p, ctx->smask.p, ctx->vabyte.p, slot_mask_dev, P.j, J, slots,
+                                      p == 0, p + 1 == passes.size(), s));
+  }
   return DLSM_OK;
 }
 

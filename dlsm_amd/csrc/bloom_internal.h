@@ -59,9 +59,37 @@ struct VFileDev {
   uint32_t smallest_len, largest_len;
   uint64_t largest_trailer;            // seq << 8 | type of the largest internal key
   FilterDev f;                         // f.data == nullptr: the table has no filter
+  uint32_t line0;                      // sliced level: the file's first line in the level image
+  uint32_t reserved;
 };
 
 constexpr int kNumLevels = 6;  // config::kNumLevels (db/dbformat.h:26)
+
+// Sliced version probe (levels whose filters outgrow an XCD's L2): the
+// level's filters' lines are stored back to back as one image (line0 per
+// file), the route pass writes each lookup's global line in that image, and a
+// partition / LDS slice / unpermute round answers all of the level's probes.
+constexpr int kVSliceLg = 11;                                  // 2^11 lines (128 KiB) per slice
+constexpr uint32_t kVMaxSlices = 1024;                         // slices per partition pass
+constexpr int kVChunk = 16384;                                 // lookups per partition chunk
+constexpr uint32_t kVRegion = kVChunk + 4u * kVMaxSlices;      // entries per chunk region
+constexpr uint32_t kVNoLine = 0xffffffffu;                     // route: no probe in this level
+constexpr uint16_t kVNoPos = 0xffffu;                          // partition: no probe in this pass
+constexpr uint32_t kVPlanBudget = 512;                         // slice-pass workgroups the entries spread over
+
+// The version's key space cut at every file bound: bnd[0, n_bnd) holds the
+// distinct 16-byte prefixes of all files' smallest and largest user keys in
+// order, and ivl[j] what Version::Get visits for a lookup whose prefix lies
+// strictly between bnd[j-1] and bnd[j] (j = 0: below all, j = n_bnd: above
+// all) -- the level-0 files holding it and each level's FindFile pick when
+// its smallest key admits the lookup.  Prefixes decide the bytewise order
+// whenever they differ, so an open interval's answers are fixed; a lookup
+// whose prefix equals a bound takes the full comparison path.
+struct VIntervalDev {
+  uint64_t l0mask;                  // bit f: level-0 file f (search order) holds the lookup
+  uint32_t pick[kNumLevels - 1];    // per level 1..5: the picked file (search order index) or ~0u
+  uint32_t reserved;
+};
 
 // Files in search order: level-0 newest first, then levels 1.. in key order.
 struct VersionDev {
@@ -75,6 +103,11 @@ struct VersionDev {
   uint32_t n_l0;
   uint32_t lvl_begin[kNumLevels];
   uint32_t lvl_count[kNumLevels];
+  int32_t lvl_sliced[kNumLevels];  // sliced level: its index j among the sliced levels, else -1
+  const ulonglong2* bnd;           // interval index (VIntervalDev)
+  const VIntervalDev* ivl;
+  uint32_t n_bnd;
+  int32_t k_all;  // the probe count every filter of the version has, or 0 when they differ
 };
 
 // Legacy-format build job.
@@ -215,6 +248,32 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
 
 hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
                                 uint64_t* slot_mask, uint32_t* level_file, hipStream_t s);
+// Route pass of the sliced version probe: launch_version_probe's outputs for
+// the levels probed directly, plus hv[i] = BloomHash and, for sliced level j,
+// gl[j * n + i] = the lookup's global line in the level image (kVNoLine: none).
+hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snapshot, uint64_t* slot_mask,
+                                uint32_t* level_file, uint32_t* hv, uint32_t* gl, hipStream_t s);
+// One partition pass: the lookups whose line g (in gl[0, n)) lies in
+// [g0, g0 + S * 2^kVSliceLg) bucketed by slice per kVChunk-lookup chunk
+// (entries: chunk regions of kVRegion, tab: chunk-major rows of S+1 u16,
+// pos: the bucketed position or kVNoPos).
+// gcnt (S u32, zero on entry, zero again on return) collects each slice's
+// entry units; plan (S+1 u32) receives the slice pass's workgroup plan.
+hipError_t launch_version_partition(const uint32_t* hv, const uint32_t* gl, uint64_t n, uint32_t g0, uint32_t S,
+                                    uint32_t* entries, uint16_t* pos, uint16_t* tab, uint32_t* gcnt,
+                                    uint32_t* plan, hipStream_t s);
+// The slice pass over `image` lines [0, L) of this pass (a 2^kVSliceLg-line
+// slice per workgroup, a slice's chunks split over its planned parts, k
+// probes per entry): answer bit 0 per entry.
+hipError_t launch_version_slices(const uint8_t* image, uint32_t L, int k, uint32_t S, uint32_t n_chunks,
+                                 const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
+                                 const uint32_t* plan, hipStream_t s);
+// Answers back to lookup order: abyte[i] gets bit jbit (written on the first
+// pass, OR-ed after); the last pass ORs every sliced level's bit into
+// slot_mask[i] at slot (slots >> 8j) & 63.
+hipError_t launch_version_unpermute(uint64_t n, const uint16_t* pos, const uint8_t* smask, uint8_t* abyte,
+                                    uint64_t* slot_mask, int jbit, int n_sliced, uint64_t slots, bool first,
+                                    bool last, hipStream_t s);
 hipError_t launch_filter_block_probe(const uint8_t* blk, uint64_t len, KeyDesc keys,
                                      const uint64_t* block_offsets, uint8_t* out, hipStream_t s);
 hipError_t launch_legacy_scatter(const LegacyJobDev* jobs, const uint64_t* key0s, int n_jobs,

@@ -1360,11 +1360,14 @@ __device__ __forceinline__ uint32_t packed_answer(uint32_t acc, uint32_t slotmap
 // LGW 0..2: packed image of a group of 1, 2 or 3-4 filters (a W-bit field per
 // bit position: 8 / 4 / 2 times the lines per slice), whose member m answers
 // in bit (slotmap >> 4m) & 7.
-template <int LGR, int LGW, int K, int NT, int C>
+// plan (nullptr: every slice has `parts` parts): S+1 workgroup starts, slice
+// s owning workgroups [plan[s], plan[s+1]) -- its parts, as many as its share
+// of the entries asks for (version_plan_kernel); workgroups past plan[S] exit.
+template <int LGR, int LGW, int K, int NT, int C, uint32_t CRE = probe_region(C)>
 __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     const uint8_t* __restrict__ stacked, uint32_t L, uint32_t Rs, uint32_t slotmap, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
-    uint8_t* __restrict__ smask, int parts) {
+    uint8_t* __restrict__ smask, int parts, const uint32_t* __restrict__ plan = nullptr) {
   // LDS holds up to R = 2^LGR lines; a slice is Rs <= R lines (Rs < R when the
   // slices are balanced so that S x parts fills the CUs exactly)
   constexpr uint32_t R = 1u << LGR;
@@ -1379,8 +1382,22 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t wi = xcd_block(blockIdx.x, gridDim.x);
-  const uint32_t s = wi % S;
-  const uint32_t p = wi / S;
+  uint32_t s, p;
+  if (plan) {
+    if (wi >= plan[S]) return;  // before any barrier: the whole workgroup leaves
+    uint32_t lo = 0, hi = S - 1;  // the slice whose workgroup range holds wi
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (plan[mid] <= wi) lo = mid;
+      else hi = mid - 1;
+    }
+    s = lo;
+    p = wi - plan[s];
+    parts = static_cast<int>(plan[s + 1] - plan[s]);
+  } else {
+    s = wi % S;
+    p = wi / S;
+  }
   const uint32_t lo_line = s * Rs;
   const uint32_t nl = min(Rs, L - lo_line);
   // The slice into LDS: every 16-byte load in flight before the first LDS
@@ -1394,7 +1411,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
   const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
-  constexpr uint32_t CRU = probe_region(C) / 4;  // chunk region stride in 16-byte units
+  constexpr uint32_t CRU = CRE / 4;  // chunk region stride in 16-byte units
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
@@ -1604,10 +1621,16 @@ __device__ __forceinline__ int cmp_prefix(const ulonglong2& a, const ulonglong2&
   return 0;
 }
 
-template <int MODE>
+// ROUTE: the sliced version probe's route pass -- a file of a sliced level
+// (v.lvl_sliced[lv] = j >= 0) is not probed here; the lookup's global line in
+// the level image goes to gl[j * n + i] instead (kVNoLine when the level has
+// no candidate or the candidate has no filter), and its hash to hv[i].
+template <int MODE, bool ROUTE = false>
 __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
                                                                uint64_t* __restrict__ slot_mask,
-                                                               uint32_t* __restrict__ level_file) {
+                                                               uint32_t* __restrict__ level_file,
+                                                               uint32_t* __restrict__ hv = nullptr,
+                                                               uint32_t* __restrict__ gl = nullptr) {
   const uint64_t i = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x;
   if (i >= kd.n) return;
   uint64_t s, l;
@@ -1644,6 +1667,7 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
   for (int lv = 1; lv < kNumLevels; lv++) {
     const uint32_t nf = v.lvl_count[lv];
     uint32_t pick = 0xffffffffu;
+    uint32_t gline = kVNoLine;
     if (nf) {
       const uint32_t b = v.lvl_begin[lv];
       // FindFile: earliest file whose largest internal key >= the lookup key
@@ -1662,12 +1686,453 @@ __global__ __launch_bounds__(kBlock) void version_probe_kernel(VersionDev v, Key
       if (vs_small(b + right) >= 0) {
         pick = right;
         const VFileDev& F = v.files[b + right];
-        if (F.f.data == nullptr || full_may_match(h, F.f)) m |= 1ull << (v.n_l0 + lv - 1);
+        if (ROUTE && v.lvl_sliced[lv] >= 0 && F.f.data != nullptr)
+          gline = F.line0 + fastmod(h, F.f.L, F.f.magic);
+        else if (F.f.data == nullptr || full_may_match(h, F.f))
+          m |= 1ull << (v.n_l0 + lv - 1);
       }
     }
     if (level_file) level_file[i * (kNumLevels - 1) + (lv - 1)] = pick;
+    if (ROUTE && v.lvl_sliced[lv] >= 0) gl[static_cast<uint64_t>(v.lvl_sliced[lv]) * kd.n + i] = gline;
   }
   slot_mask[i] = m;
+  if (ROUTE) hv[i] = h;
+}
+
+// The version probe with the version's interval index in LDS (a persistent
+// grid: each workgroup copies it once).  A lookup finds its open interval
+// with one branchless binary search over the bound prefixes (VersionDev::bnd)
+// and reads which level-0 files hold it and each level's FindFile pick from
+// the interval's record: the reference's per-level searches and level-0
+// range checks (Version::ForEachOverlapping, db/version_set.cc:273-321) are
+// resolved once per version, at dlsm_version_create, instead of per lookup.
+// A lookup whose prefix equals a bound prefix (it equals a file's smallest /
+// largest user key, or shares 16 bytes with one) takes the full comparison
+// path, including FindFile's internal-key tie-break on the snapshot.
+// ROUTE as in version_probe_kernel.
+//
+// Direct probes (level-0 files, and levels probed directly) do not run where
+// a lane finds them: a scattered load costs the vector memory pipeline about
+// one cycle per cache line it touches whatever the exec mask, and each probe
+// site of a lane-per-lookup loop is a chain of up to k such loads with most
+// lanes idle.  Instead every lane appends its probe tasks (file, slot, lane)
+// to a wave-private queue in LDS, and the wave answers them 64 at a time:
+// the task lines are fetched four lanes per line, each lane one 16-byte
+// quarter -- so one load instruction covers 16 whole lines -- and staged in
+// LDS, then every lane tests its own task's k bits there and ORs the answer
+// into the owning lane's slot mask (LDS).
+struct VMeta {  // 32 B per file
+  const uint8_t* data;
+  uint32_t L, magic, line0;
+  int32_t k, lg;
+  uint32_t pad;
+};
+constexpr int kVRouteNT = 1024;           // 16 waves, one workgroup per CU (the LDS below)
+constexpr int kVRouteWaves = kVRouteNT / 64;
+constexpr int kVRound = 128;              // tasks per round: two 64-line halves' loads in flight
+constexpr int kVQueue = kVRound + 64;     // queued probe tasks per wave (one enqueue adds <= 64)
+// per wave: staged task lines (one half) | task line addresses | task queue |
+// owning lanes' hashes | their answer masks
+constexpr size_t kVWaveLds = 64 * 64 + kVRound * 8 + kVQueue * 4 + 64 * 4 + 64 * 8;
+constexpr size_t kVLdsMax = 160u * 1024u;  // the CU's LDS
+
+size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf) {
+  return static_cast<size_t>(n_bnd) * 16u + (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev) +
+         static_cast<size_t>(nf) * sizeof(VMeta) + kVRouteWaves * kVWaveLds;
+}
+
+// FullFilterBlockReader::KeyMayMatch (full_filter_block.cc:269-284) for one
+// lane (files whose "lines" are not 64 bytes: the reader's log2 0 branch).
+__device__ __forceinline__ uint32_t full_may_match_all(uint32_t h, const VMeta& f) {
+  FilterDev g{f.data, f.L, f.magic, f.k, f.lg};
+  return full_may_match(h, g);
+}
+
+template <int MODE, bool ROUTE, int K>
+__global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
+                                                                uint64_t* __restrict__ slot_mask,
+                                                                uint32_t* __restrict__ level_file,
+                                                                uint32_t* __restrict__ hv, uint32_t* __restrict__ gl,
+                                                                uint32_t nf) {
+  extern __shared__ uint4 vdyn[];
+  const uint32_t nb = v.n_bnd;
+  ulonglong2* bnd = reinterpret_cast<ulonglong2*>(vdyn);
+  VIntervalDev* ivl = reinterpret_cast<VIntervalDev*>(bnd + nb);
+  VMeta* meta = reinterpret_cast<VMeta*>(ivl + nb + 1);
+  const uint32_t lane = threadIdx.x & 63u;
+  const int wv = wave_id();
+  uint8_t* wl = reinterpret_cast<uint8_t*>(meta + nf) + static_cast<size_t>(wv) * kVWaveLds;
+  typedef __attribute__((address_space(3))) uint32_t lds32;
+  typedef __attribute__((address_space(3))) unsigned long long lds64;
+  lds32* st = (lds32*)reinterpret_cast<uint32_t*>(wl);                                // 64 lines of 64 B
+  lds64* ad = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096);              // kVRound line addresses
+  lds32* tq = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8);
+  lds32* hb = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8 + kVQueue * 4);
+  lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVRound * 8 + kVQueue * 4 + 64 * 4);
+  for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) bnd[f] = v.bnd[f];
+  for (uint32_t f = threadIdx.x; f <= nb; f += kVRouteNT) ivl[f] = v.ivl[f];
+  for (uint32_t f = threadIdx.x; f < nf; f += kVRouteNT) {
+    const VFileDev& F = v.files[f];
+    meta[f] = VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
+  }
+  mb[lane] = 0ull;
+  __syncthreads();
+  const uint64_t tnum = (snapshot << 8) | 1u;  // LookupKey(user_key, snapshot): kValueTypeForSeek
+  // One round: tasks tq[0, n), n <= kVRound, wave-uniform.  Lane t computes
+  // the line addresses of tasks t and t + 64; every line is fetched four lanes
+  // per line (lane & 3 = its 16-byte quarter), both halves' loads in flight
+  // at once; each half is staged in LDS in turn and lane t tests its task's
+  // k bits there.
+  auto round = [&](uint32_t n) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    uint32_t task[2], h[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+      const uint32_t t = lane + 64u * hf;
+      task[hf] = t < n ? tq[t] : ~0u;
+      h[hf] = 0u;
+      if (task[hf] != ~0u) {
+        const VMeta& F = meta[task[hf] & 0xffffu];
+        h[hf] = hb[task[hf] >> 26];
+        ad[t] = reinterpret_cast<unsigned long long>(F.data + (fastmod(h[hf], F.L, F.magic) << 6));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const uint32_t qq = lane & 3u;
+    uint4 qv[8];
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+      const uint32_t t = 16u * r + (lane >> 2);
+      qv[r] = make_uint4(0u, 0u, 0u, 0u);
+      if (t < n) qv[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ad[t]) + 16u * qq);
+    }
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) {
+      if (64u * hf >= n) break;  // wave-uniform
+#pragma unroll
+      for (int r = 4 * hf; r < 4 * hf + 4; r++) {
+        const uint32_t t = 16u * r + (lane >> 2);
+        if (t < n) {
+          lds32* d = st + (t - 64u * hf) * 16u + qq * 4u;
+          d[0] = qv[r].x;
+          d[1] = qv[r].y;
+          d[2] = qv[r].z;
+          d[3] = qv[r].w;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      if (task[hf] != ~0u) {
+        // HashMayMatchPrepared, bloom_impl.h:466-479, on the staged line
+        const lds32* line = st + lane * 16u;
+        uint32_t hh = h[hf];
+        const uint32_t delta = bloom_delta(hh);
+        uint32_t bad = 0u;
+        if constexpr (K > 0) {
+#pragma unroll
+          for (int q = 0; q < K; q++, hh += delta) bad |= ~line[(hh & 511u) >> 5] >> (hh & 31u);
+        } else {
+          const int kk = meta[task[hf] & 0xffffu].k;
+          for (int q = 0; q < kk; q++, hh += delta) bad |= ~line[(hh & 511u) >> 5] >> (hh & 31u);
+        }
+        if (!(bad & 1u)) atomicOr((unsigned long long*)&mb[task[hf] >> 26], 1ull << ((task[hf] >> 16) & 63u));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+  };
+  const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kVRouteWaves * 64u;
+  for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kVRouteWaves + wv) * 64u; base < kd.n; base += wstride) {
+    const uint64_t i = base + lane;
+    const bool live = i < kd.n;
+    const uint64_t ii = live ? i : kd.n - 1;  // a dead lane reads a valid key and stores nothing
+    uint64_t s, l;
+    if (kd.offsets) {
+      s = kd.offsets[ii];
+      l = kd.offsets[ii + 1] - s;
+    } else {
+      s = ii * kd.key_len;
+      l = kd.key_len;
+    }
+    l = l > kd.suffix ? l - kd.suffix : 0;  // ExtractUserKey
+    const uint8_t* uk = kd.bytes + s;
+    uint32_t h;
+    ulonglong2 q;
+    if constexpr (MODE == KM_K20) {  // one read of the key's five words: hash and prefix
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(uk);
+      uint32_t x[5];
+#pragma unroll
+      for (int j = 0; j < 5; j++) x[j] = __builtin_nontemporal_load(w + j);
+      h = hash_init(20, kBloomSeed);
+#pragma unroll
+      for (int j = 0; j < 5; j++) h = hash_word(h, x[j]);
+      q.x = (static_cast<uint64_t>(__builtin_bswap32(x[0])) << 32) | __builtin_bswap32(x[1]);
+      q.y = (static_cast<uint64_t>(__builtin_bswap32(x[2])) << 32) | __builtin_bswap32(x[3]);
+    } else {
+      h = key_hash<MODE>(kd, ii);
+      q = key_prefix<MODE>(uk, l);
+    }
+    hb[lane] = h;
+    // the open interval: j = bounds below the lookup's prefix (a lower bound
+    // whose halving steps depend on nb only: the same for every lane)
+    uint32_t j = 0;
+    if (nb) {
+      uint32_t len = nb;
+      while (len > 1) {
+        const uint32_t half = len >> 1;
+        const ulonglong2 p = bnd[j + half - 1];
+        if (p.x < q.x || (p.x == q.x && p.y < q.y)) j += half;
+        len -= half;
+      }
+      const ulonglong2 p = bnd[j];
+      if (p.x < q.x || (p.x == q.x && p.y < q.y)) j++;
+    }
+    const bool exact = j < nb && bnd[j].x == q.x && bnd[j].y == q.y;
+    uint64_t l0m;
+    uint32_t pick[kNumLevels - 1];
+    if (!exact) {
+      const VIntervalDev& R = ivl[j];
+      l0m = R.l0mask;
+#pragma unroll
+      for (int lv = 0; lv < kNumLevels - 1; lv++) pick[lv] = R.pick[lv];
+    } else {
+      // the full comparisons (version_probe_kernel's), tables in global memory
+      auto vs_small = [&](uint32_t f) {
+        const int r = cmp_prefix(q, v.pre_small[f]);
+        return r ? r : bytewise_cmp(uk, l, v.keyblob + v.files[f].smallest_off, v.files[f].smallest_len);
+      };
+      auto vs_large = [&](uint32_t f) {
+        const int r = cmp_prefix(q, v.pre_large[f]);
+        return r ? r : bytewise_cmp(uk, l, v.keyblob + v.files[f].largest_off, v.files[f].largest_len);
+      };
+      l0m = 0;
+      for (uint32_t f = 0; f < v.n_l0; f++)
+        if (vs_small(f) >= 0 && vs_large(f) <= 0) l0m |= 1ull << f;
+      for (int lv = 1; lv < kNumLevels; lv++) {
+        pick[lv - 1] = 0xffffffffu;
+        const uint32_t nf_l = v.lvl_count[lv];
+        if (!nf_l) continue;
+        const uint32_t b = v.lvl_begin[lv];
+        uint32_t left = 0, right = nf_l - 1;
+        while (left < right) {
+          const uint32_t mid = (left + right) / 2;
+          int r = -vs_large(b + mid);
+          if (r == 0) {
+            const uint64_t tr = v.files[b + mid].largest_trailer;
+            r = tr > tnum ? -1 : (tr < tnum ? 1 : 0);
+          }
+          if (r < 0) left = mid + 1;
+          else right = mid;
+        }
+        if (vs_small(b + right) >= 0) pick[lv - 1] = b + right;
+      }
+    }
+    if (!live) l0m = 0;
+    uint64_t m = 0;
+    uint32_t queued = 0;  // wave-uniform
+    // a direct probe of file f for slot `slot` (this lane, if `want`): queued;
+    // a full queue answers a round of 64
+    auto enqueue = [&](bool want, uint32_t f, uint32_t slot) {
+      const uint64_t b = __ballot(want);
+      if (!b) return;
+      if (want) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
+        tq[queued + below] = (lane << 26) | (slot << 16) | f;
+      }
+      queued += static_cast<uint32_t>(__builtin_popcountll(b));
+      if (queued >= static_cast<uint32_t>(kVRound)) {
+        round(kVRound);
+        const uint32_t rest = queued - kVRound;  // move the overflow (< 64) to the front
+        const uint32_t t = lane < rest ? tq[kVRound + lane] : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < rest) tq[lane] = t;
+        queued = rest;
+      }
+    };
+    const uint64_t anyl0 = uniform64(__ballot(l0m != 0));
+    for (uint32_t f = 0; anyl0 && f < v.n_l0; f++) {  // level 0: newest first
+      const bool in = (l0m >> f) & 1u;
+      const VMeta& F = meta[f];
+      if (in && F.data == nullptr) m |= 1ull << f;
+      if (in && F.data != nullptr && F.lg != 6 && full_may_match_all(h, F)) m |= 1ull << f;  // rare: 1-byte lines
+      enqueue(in && F.data != nullptr && F.lg == 6, f, f);
+    }
+    for (int lv = 1; lv < kNumLevels; lv++) {
+      const uint32_t slot = v.n_l0 + lv - 1;
+      const uint32_t pf = live && v.lvl_count[lv] ? pick[lv - 1] : 0xffffffffu;
+      uint32_t gline = kVNoLine;
+      bool task = false;
+      if (pf != 0xffffffffu) {
+        const VMeta& F = meta[pf];
+        if (ROUTE && v.lvl_sliced[lv] >= 0 && F.data != nullptr) {
+          gline = F.line0 + fastmod(h, F.L, F.magic);
+        } else if (F.data == nullptr) {
+          m |= 1ull << slot;
+        } else if (F.lg != 6) {
+          if (full_may_match_all(h, F)) m |= 1ull << slot;
+        } else {
+          task = true;
+        }
+      }
+      enqueue(task, pf, slot);
+      if (live && level_file)
+        level_file[i * (kNumLevels - 1) + (lv - 1)] = pf == 0xffffffffu ? pf : pf - v.lvl_begin[lv];
+      if (ROUTE && live && v.lvl_sliced[lv] >= 0) gl[static_cast<uint64_t>(v.lvl_sliced[lv]) * kd.n + i] = gline;
+    }
+    if (queued) round(queued);
+    m |= mb[lane];
+    mb[lane] = 0ull;
+    if (live) {
+      slot_mask[i] = m;
+      if (ROUTE) hv[i] = h;
+    }
+  }
+}
+
+// Sliced version probe, partition pass (one NT-thread workgroup per chunk of
+// kVChunk lookups): each lookup whose global line g lies in this pass's
+// slices [g0, g0 + S << kVSliceLg) gets the entry probe_entry(h, line offset
+// in its slice), bucketed by slice inside the chunk's region, every bucket
+// padded to whole 16-byte units (the slice pass's unit); pos[i] = the entry's
+// position in the region, kVNoPos for a lookup without a probe in this pass.
+template <int NT>
+__global__ __launch_bounds__(NT) void version_partition_kernel(const uint32_t* __restrict__ hv,
+                                                               const uint32_t* __restrict__ gl, uint64_t n,
+                                                               uint32_t g0, uint32_t S,
+                                                               uint32_t* __restrict__ entries,
+                                                               uint16_t* __restrict__ pos,
+                                                               uint16_t* __restrict__ tab,
+                                                               uint32_t* __restrict__ gcnt) {
+  constexpr int C = kVChunk;
+  constexpr int PER = C / NT;
+  __shared__ __attribute__((aligned(16))) uint32_t stage[kVRegion];
+  __shared__ uint32_t hist[kVMaxSlices + 1];
+  __shared__ uint8_t npad[kVMaxSlices];
+  __shared__ uint32_t wsum[NT / 64];
+  const int tid = threadIdx.x;
+  const uint32_t c = blockIdx.x;
+  const uint64_t first = static_cast<uint64_t>(c) * C;
+  const uint32_t nk = static_cast<uint32_t>(min(static_cast<uint64_t>(C), n - first));
+  for (uint32_t b = tid; b <= S; b += NT) hist[b] = 0;
+  uint32_t e[PER], sr[PER];  // entry; slice << 16 | rank (~0: no probe)
+#pragma unroll
+  for (int r = 0; r < PER; r++) {  // coalesced dword loads, all in flight before the barrier
+    const uint32_t i = r * NT + tid;
+    e[r] = i < nk ? __builtin_nontemporal_load(hv + first + i) : 0u;
+    sr[r] = i < nk ? __builtin_nontemporal_load(gl + first + i) : kVNoLine;
+  }
+  __syncthreads();
+  const uint32_t span = S << kVSliceLg;
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const uint32_t d = sr[r] - g0;
+    if (sr[r] != kVNoLine && d < span) {
+      const uint32_t sl = d >> kVSliceLg;
+      sr[r] = (sl << 16) | atomicAdd(&hist[sl], 1u);
+      e[r] = probe_entry(e[r], d & ((1u << kVSliceLg) - 1u));
+    } else {
+      sr[r] = ~0u;
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = tid; b < S; b += NT) {  // whole 16-byte units
+    const uint32_t pad = (0u - hist[b]) & 3u;
+    npad[b] = static_cast<uint8_t>(pad);
+    hist[b] += pad;
+    if (hist[b]) atomicAdd(&gcnt[b], hist[b] >> 2);  // the slice's units, for the slice pass's plan
+  }
+  __syncthreads();
+  const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
+  for (uint32_t b = tid; b <= S; b += NT) tab[static_cast<uint64_t>(c) * (S + 1) + b] = static_cast<uint16_t>(hist[b]);
+  // padding entries (bit 31 set: never answered) at the end of every bucket;
+  // the bucket's own entries fill the rest below
+  for (uint32_t b = tid; b < S; b += NT) {
+    const uint32_t end = hist[b + 1];
+    for (uint32_t q = end - npad[b]; q < end; q++) stage[q] = kProbePadEntry;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < PER; r++) {
+    const uint32_t i = r * NT + tid;
+    if (i >= nk) continue;
+    uint16_t p = kVNoPos;
+    if (sr[r] != ~0u) {
+      const uint32_t q = hist[sr[r] >> 16] + (sr[r] & 0xffffu);
+      stage[q] = e[r];
+      p = static_cast<uint16_t>(q);
+    }
+    pos[first + i] = p;
+  }
+  __syncthreads();
+  store_chunk_u32<NT, true>(entries + static_cast<uint64_t>(c) * kVRegion, stage, total);
+}
+
+// Sliced version probe, slice plan (one workgroup): every slice gets
+// max(1, ceil(units / target)) workgroup parts, target = the pass's units
+// spread over `budget` parts (at least kVMinPartUnits), so a slice that
+// draws a large share of the lookups -- the last file of a level takes every
+// key past the level's range (FindFile's quirk) -- is walked by many
+// workgroups instead of one.  plan = exclusive prefix of the parts (S+1
+// entries); the counters are zeroed for the next pass.
+constexpr uint32_t kVMinPartUnits = 4096;
+__global__ __launch_bounds__(1024) void version_plan_kernel(uint32_t* __restrict__ gcnt, uint32_t S, uint32_t budget,
+                                                            uint32_t* __restrict__ plan) {
+  __shared__ uint32_t a[kVMaxSlices + 1];
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t tot;
+  const int tid = threadIdx.x;
+  uint32_t c = 0;
+  if (static_cast<uint32_t>(tid) < S) {
+    c = gcnt[tid];
+    gcnt[tid] = 0;
+  }
+  const uint32_t sum = wave_sum(c);
+  if ((tid & 63) == 0) wsum[tid >> 6] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < 16; w++) t += wsum[w];
+    tot = t;
+  }
+  __syncthreads();
+  const uint32_t target = max(kVMinPartUnits, (tot + budget - 1) / budget);
+  if (static_cast<uint32_t>(tid) < S) a[tid] = max(1u, (c + target - 1) / target);
+  if (tid == 0) a[S] = 0;
+  __syncthreads();
+  block_excl_scan_lds<1024>(a, static_cast<int>(S + 1), wsum);
+  for (uint32_t b = tid; b <= S; b += 1024) plan[b] = a[b];
+}
+
+// Sliced version probe, unpermute (one workgroup per chunk): the chunk's
+// answers (bit 0 of each answer byte, at the entries' positions) staged in
+// LDS, then per lookup its answer -- 0 without a probe in this pass -- into
+// abyte bit jbit (written by the first pass, OR-ed by later ones); the last
+// pass folds every sliced level's bit into slot_mask at its slot.
+__global__ __launch_bounds__(kBlock) void version_unpermute_kernel(uint64_t n, const uint16_t* __restrict__ pos,
+                                                                   const uint8_t* __restrict__ smask,
+                                                                   uint8_t* __restrict__ abyte,
+                                                                   uint64_t* __restrict__ slot_mask, int jbit,
+                                                                   int n_sliced, uint64_t slots, int first,
+                                                                   int last) {
+  __shared__ __attribute__((aligned(16))) uint8_t sm[kVRegion];
+  const int tid = threadIdx.x;
+  const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kVChunk;
+  const uint32_t nk = static_cast<uint32_t>(min(static_cast<uint64_t>(kVChunk), n - base));
+  const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(blockIdx.x) * kVRegion);
+  for (uint32_t v = tid; v < kVRegion / 16u; v += kBlock) reinterpret_cast<uint4*>(sm)[v] = s4[v];
+  __syncthreads();
+  for (uint32_t i = tid; i < nk; i += kBlock) {
+    const uint16_t p = pos[base + i];
+    const uint32_t bit = p == kVNoPos ? 0u : (sm[p] & 1u);
+    uint32_t a = bit << jbit;
+    if (!first) a |= abyte[base + i];
+    if (!last) {
+      abyte[base + i] = static_cast<uint8_t>(a);
+      continue;
+    }
+    uint64_t m = slot_mask[base + i];
+    for (int j = 0; j < n_sliced; j++) m |= static_cast<uint64_t>((a >> j) & 1u) << ((slots >> (8 * j)) & 63u);
+    slot_mask[base + i] = m;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2446,15 +2911,107 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
   return hipGetLastError();
 }
 
+
+hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snapshot, uint64_t* slot_mask,
+                                uint32_t* level_file, uint32_t* hv, uint32_t* gl, hipStream_t s) {
+  if (keys.n == 0) return hipSuccess;
+  const bool k20 = keys.offsets == nullptr && keys.key_len == 20 && keys.suffix == 0 &&
+                   (reinterpret_cast<uintptr_t>(keys.bytes) & 3u) == 0;
+  const bool route = hv != nullptr;
+  uint32_t nf = v.n_l0;
+  for (int lv = 1; lv < kNumLevels; lv++) nf = std::max(nf, v.lvl_begin[lv] + v.lvl_count[lv]);
+  // $DLSM_VERSION_LDS=0: the global-table kernel (A/B)
+  static const bool lds_ok = [] {
+    const char* e = getenv("DLSM_VERSION_LDS");
+    return !(e && atoi(e) == 0);
+  }();
+  const size_t lds = version_lds_bytes(v.n_bnd, nf);
+  if (lds_ok && lds <= kVLdsMax) {
+    // all files probed directly or through the queue share one probe count
+    // in the common case (one bits_per_key): k = 6 unrolled
+    bool k6 = true;
+    (void)k6;
+    const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((keys.n + kVRouteNT - 1) / kVRouteNT,
+                                                                static_cast<uint64_t>(device_cus())));
+#define DLSM_VLDS(MM, RR, KK)                                                                                   \
+  do {                                                                                                          \
+    static bool attr = false;                                                                                   \
+    if (!attr) {                                                                                                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&version_lds_kernel<MM, RR, KK>),                 \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kVLdsMax));       \
+      attr = true;                                                                                              \
+    }                                                                                                           \
+    version_lds_kernel<MM, RR, KK><<<g, kVRouteNT, lds, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl, nf); \
+  } while (0)
+    if (v.k_all == 6) {
+      if (k20 && route) DLSM_VLDS(KM_K20, true, 6);
+      else if (k20) DLSM_VLDS(KM_K20, false, 6);
+      else if (route) DLSM_VLDS(KM_GENERIC, true, 6);
+      else DLSM_VLDS(KM_GENERIC, false, 6);
+    } else {
+      if (k20 && route) DLSM_VLDS(KM_K20, true, 0);
+      else if (k20) DLSM_VLDS(KM_K20, false, 0);
+      else if (route) DLSM_VLDS(KM_GENERIC, true, 0);
+      else DLSM_VLDS(KM_GENERIC, false, 0);
+    }
+#undef DLSM_VLDS
+    return hipGetLastError();
+  }
+  const unsigned g = static_cast<unsigned>((keys.n + kBlock - 1) / kBlock);
+  if (k20 && route)
+    version_probe_kernel<KM_K20, true><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl);
+  else if (k20)
+    version_probe_kernel<KM_K20, false><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+  else if (route)
+    version_probe_kernel<KM_GENERIC, true><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl);
+  else
+    version_probe_kernel<KM_GENERIC, false><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+  return hipGetLastError();
+}
+
 hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
                                 uint64_t* slot_mask, uint32_t* level_file, hipStream_t s) {
-  if (keys.n == 0) return hipSuccess;
-  const unsigned g = static_cast<unsigned>((keys.n + kBlock - 1) / kBlock);
-  if (keys.offsets == nullptr && keys.key_len == 20 && keys.suffix == 0 &&
-      (reinterpret_cast<uintptr_t>(keys.bytes) & 3u) == 0)
-    version_probe_kernel<KM_K20><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+  return launch_version_route(v, keys, snapshot, slot_mask, level_file, nullptr, nullptr, s);
+}
+
+constexpr int kVPartNT = 1024;
+
+hipError_t launch_version_partition(const uint32_t* hv, const uint32_t* gl, uint64_t n, uint32_t g0, uint32_t S,
+                                    uint32_t* entries, uint16_t* pos, uint16_t* tab, uint32_t* gcnt,
+                                    uint32_t* plan, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (S < 1 || S > kVMaxSlices) return hipErrorInvalidValue;
+  const unsigned nC = static_cast<unsigned>((n + kVChunk - 1) / kVChunk);
+  version_partition_kernel<kVPartNT><<<nC, kVPartNT, 0, s>>>(hv, gl, n, g0, S, entries, pos, tab, gcnt);
+  version_plan_kernel<<<1, 1024, 0, s>>>(gcnt, S, kVPlanBudget, plan);
+  return hipGetLastError();
+}
+
+hipError_t launch_version_slices(const uint8_t* image, uint32_t L, int k, uint32_t S, uint32_t n_chunks,
+                                 const uint32_t* entries, const uint16_t* tab, uint8_t* smask,
+                                 const uint32_t* plan, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  if (S < 1 || S > kVMaxSlices || L == 0) return hipErrorInvalidValue;
+  constexpr int NT = DLSM_PROBE_NT;
+  constexpr uint32_t R = 1u << kVSliceLg;
+  const uint32_t grid = S + kVPlanBudget;  // >= the plan's parts: sum max(1, ceil(u / target)) <= S + budget
+  // packed image of one member (LGW 0): the filters' own line bytes, answer in bit 0
+  if (k == 6)
+    probe_slice_kernel<kVSliceLg, 0, 6, NT, kVChunk, kVRegion><<<grid, NT, 0, s>>>(
+        image, L, R, 0u, k, S, n_chunks, entries, tab, smask, 1, plan);
   else
-    version_probe_kernel<KM_GENERIC><<<g, kBlock, 0, s>>>(v, keys, snapshot, slot_mask, level_file);
+    probe_slice_kernel<kVSliceLg, 0, 0, NT, kVChunk, kVRegion><<<grid, NT, 0, s>>>(
+        image, L, R, 0u, k, S, n_chunks, entries, tab, smask, 1, plan);
+  return hipGetLastError();
+}
+
+hipError_t launch_version_unpermute(uint64_t n, const uint16_t* pos, const uint8_t* smask, uint8_t* abyte,
+                                    uint64_t* slot_mask, int jbit, int n_sliced, uint64_t slots, bool first,
+                                    bool last, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const unsigned nC = static_cast<unsigned>((n + kVChunk - 1) / kVChunk);
+  version_unpermute_kernel<<<nC, kBlock, 0, s>>>(n, pos, smask, abyte, slot_mask, jbit, n_sliced, slots,
+                                                 first ? 1 : 0, last ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -190,7 +190,13 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             streams (default 0, or $DLSM_PROBE_SERIAL)
  *   DLSM_OPT_FAULT_INJECT     test hook: v > 0 makes every build and probe call on the
  *                             context return -v (4 = DLSM_E_DEVICE, 5 = DLSM_E_NOMEM)
- *                             before touching the device; 0 (default) off */
+ *                             before touching the device; 0 (default) off
+ *   DLSM_OPT_VERSION_SLICE_BYTES  dlsm_version_create on this context: a level >= 1 whose
+ *                             filters hold more bytes goes to the sliced version probe
+ *                             (0: default 256 MiB or $DLSM_VERSION_SLICE_MIN_BYTES;
+ *                             UINT64_MAX: never)
+ *   DLSM_OPT_VERSION_PASS_SLICES  128 KiB slices per partition pass of the sliced version
+ *                             probe, 1..1024 (default 1024; larger levels take several) */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2
@@ -199,6 +205,8 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_BUILD_EXACT 5
 #define DLSM_OPT_PROBE_ROUND_SERIAL 6
 #define DLSM_OPT_FAULT_INJECT 7
+#define DLSM_OPT_VERSION_SLICE_BYTES 8
+#define DLSM_OPT_VERSION_PASS_SLICES 9
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 /* The current value of an option (so a caller can restore it). */
 int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);

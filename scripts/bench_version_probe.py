@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--space", type=int, default=100_000_000, help="key space V")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--check", type=int, default=200_000, help="lookups checked against the oracle")
+    ap.add_argument("--paths", default="both", choices=["both", "sliced", "direct"])
+    ap.add_argument("--pass-slices", type=int, default=0, help="DLSM_OPT_VERSION_PASS_SLICES (0: default)")
+    ap.add_argument("--slice-bytes", type=int, default=0, help="DLSM_OPT_VERSION_SLICE_BYTES (0: default)")
     args = ap.parse_args()
 
     import numpy as np
@@ -44,6 +47,10 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream)
+    if args.pass_slices:
+        ctx.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, args.pass_slices)
+    if args.slice_bytes:
+        ctx.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, args.slice_bytes)
     V = args.space
     key = lambda v: W.dbbench_keys_np(np.array([v], dtype=np.uint64)).tobytes()  # noqa: E731
 
@@ -85,18 +92,9 @@ def main():
     qk = dlsm_amd.Keys(W.dbbench_keys_torch(qv), Q, 20)
     mask = torch.zeros(Q, dtype=torch.int64, device=dev)
     snap = (1 << 56) - 1
-    ctx.version_probe_dev(ver, qk, snap, mask)
-    ctx.sync()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(args.reps):
-        ctx.version_probe_dev(ver, qk, snap, mask)
-    e1.record(stream)
-    stream.synchronize()
-    ms = e0.elapsed_time(e1) / args.reps
     res = {"what": "version probe (batched Get over a version), device-resident",
-           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt_bytes, "lookups": Q,
-           "ms": round(ms, 3), "mgets_s": round(Q / ms / 1e3, 1)}
+           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt_bytes, "lookups": Q}
+    want = None
     if args.check:
         import oracle
 
@@ -106,9 +104,28 @@ def main():
                           f.filter.cpu().numpy().tobytes()) for f in files]
         hq = qk.data[: n * 20].cpu().numpy()
         want, _ = oracle.version_probe(hf, hq, n, snapshot=snap)
-        got = mask[:n].cpu().numpy().astype(np.uint64)
         res["oracle_checked"] = n
-        res["matches_oracle"] = bool(np.array_equal(got, np.asarray(want, dtype=np.uint64)))
+    # path 0: levels whose filters outgrow an XCD's L2 take the sliced probe
+    # (route / partition / LDS slice / unpermute); path 1: every level direct
+    for path, label in ((0, "sliced"), (1, "direct")):
+        if args.paths != "both" and args.paths != label:
+            continue
+        ctx.set_path(path)
+        ctx.version_probe_dev(ver, qk, snap, mask)
+        ctx.sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.reps):
+            ctx.version_probe_dev(ver, qk, snap, mask)
+        e1.record(stream)
+        stream.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        rec = {"ms": round(ms, 3), "mgets_s": round(Q / ms / 1e3, 1)}
+        if want is not None:
+            got = mask[: res["oracle_checked"]].cpu().numpy().astype(np.uint64)
+            rec["matches_oracle"] = bool(np.array_equal(got, np.asarray(want, dtype=np.uint64)))
+        res[label] = rec
+    ctx.set_path(0)
     print(json.dumps(res), flush=True)
 
 

@@ -132,6 +132,7 @@ def test_bench_two_gpus_rehearsed():
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["launch"].startswith("threads")
     assert line["config"]["devices"] == [0, 0] and line["config"]["rehearsal"]
+    assert line["rehearsed"] is True and line["physical_devices"] == 1
     assert line["config"]["gpu_tables"] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
     assert line["config"]["gpu_lookups"] == [[0, 2_000_000], [2_000_000, 4_000_000]]
     assert line["value"] > 0 and line["roofline"]["achieved"] > 0
@@ -154,6 +155,7 @@ def test_bench_one_gpu_native_and_python_loop():
         assert r.returncode == 0, r.stderr[-3000:]
         line = json.loads(r.stdout.strip().splitlines()[-1])
         assert line["n_gpus"] == 1 and line["config"]["timed_by"].startswith(timed_by)
+        assert line["rehearsed"] is False and line["physical_devices"] == 1
         assert line["value"] > 0 and line["probe"]["ms"] > 0 and line["build"]["ms"] > 0
         assert line["roofline"]["hbm_read_GBs_measured"] > 1000
 
@@ -183,6 +185,7 @@ def test_bench_under_launcher_two_ranks_rehearsed():
     assert len(lines) == 1, r.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["rehearsed"] is True and line["physical_devices"] == 1  # two ranks on one GPU
     assert line["config"]["timed_by"].startswith("dlsm_multi_device_run")
     assert line["config"]["rank0_tables"] == list(range(0, 16, 2))
     assert line["config"]["rank0_lookups"] == 2_000_000

@@ -197,3 +197,91 @@ def test_gpu_version_probe_prefix_ties(gpu):
         assert np.array_equal(mask.cpu().numpy().view(np.uint64), want), snap
         assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf), snap
         v.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pass_slices", [1024, 3, 1])
+def test_gpu_version_probe_sliced(gpu, pass_slices):
+    """The sliced version probe (route pass; per sliced level a partition /
+    LDS slice / unpermute round) against the oracle: every level with filters
+    forced onto it (DLSM_OPT_VERSION_SLICE_BYTES = 1), one level with a
+    different probe count left on the direct path, a level with a file
+    without a filter, and groups of 1024, 3 or 1 slices per pass (several
+    passes per level: answer bits OR-ed across passes before the last one
+    folds them into the slot mask).  Level files and masks must equal the
+    oracle's and the direct path's."""
+    import torch
+
+    import dlsm_amd
+
+    files = make_version(6)
+    # level 4's two files at 14 bits/key (k = 9): a level of mixed k stays direct
+    rebuilt = []
+    for f in files:
+        if f.level == 4 and f.number % 2 == 0:
+            lo = int.from_bytes(f.smallest[:8], "big")
+            hi = int.from_bytes(f.largest[:8], "big")
+            vals = np.arange(lo, hi + 1, 11, dtype=np.uint64)
+            keys = oracle.keys_from_values(vals)
+            f = VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer,
+                            oracle.full_build(keys, len(vals), bpk=14))
+        rebuilt.append(f)
+    files = rebuilt
+    n = 300_007
+    q = lookups(n, 17)
+    snap = 1 << 44
+    want, want_lf = oracle.version_probe(files, q, n, snap)
+    qk = dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20)
+    old = gpu.get_option(dlsm_amd.OPT_VERSION_SLICE_BYTES)
+    try:
+        gpu.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, 1)
+        gpu.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, pass_slices)
+        v = gpu.version(files)
+        for path in (0, 1):  # sliced, then the direct kernel on the same version
+            gpu.set_path(path)
+            mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+            lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+            gpu.version_probe_dev(v, qk, snap, mask, lf)
+            gpu.sync()
+            assert np.array_equal(mask.cpu().numpy().view(np.uint64), want), (pass_slices, path)
+            assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf), (pass_slices, path)
+        v.close()
+    finally:
+        gpu.set_path(0)
+        gpu.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, old)
+        gpu.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, 1024)
+
+
+@pytest.mark.gpu
+def test_gpu_version_probe_sliced_internal_var_keys(gpu):
+    """Variable-length internal keys (suffix 8, generic route loader) through
+    the sliced probe."""
+    import torch
+
+    import dlsm_amd
+
+    files = make_version(8, with_nofilter=False)
+    n = 40_000
+    q = lookups(n, 3)
+    ikeys = [q[20 * i: 20 * i + 20].tobytes()[: 12 + i % 9] + ((77 << 8) | 1).to_bytes(8, "little")
+             for i in range(n)]
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(k) for k in ikeys])
+    data = np.frombuffer(b"".join(ikeys) + b"\0" * 16, dtype=np.uint8).copy()
+    want, want_lf = oracle.version_probe(files, data, n, 1 << 30, offsets=offs, suffix=8)
+    old = gpu.get_option(dlsm_amd.OPT_VERSION_SLICE_BYTES)
+    try:
+        gpu.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, 1)
+        gpu.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, 2)
+        v = gpu.version(files)
+        mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+        lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+        ks = dlsm_amd.Keys(torch.from_numpy(data).cuda(), n, 0, torch.from_numpy(offs).cuda(), suffix_len=8)
+        gpu.version_probe_dev(v, ks, 1 << 30, mask, lf)
+        gpu.sync()
+        assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+        assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+        v.close()
+    finally:
+        gpu.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, old)
+        gpu.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, 1024)
