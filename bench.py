@@ -107,6 +107,10 @@ def main():
                          "(the default for --gpus N > 1; at N = 1 the Python loop is the default)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-version", action="store_true",
+                    help="skip the MultiGet-style version probe leg (SURVEY §8f row 3)")
+    ap.add_argument("--no-mixed", action="store_true",
+                    help="skip the mixed-size filter set probe leg")
     ap.add_argument("--no-legacy", action="store_true",
                     help="skip the legacy-format leg (util/bloom.cc CreateFilter over the same tables)")
     args = ap.parse_args()
@@ -432,6 +436,13 @@ def main():
             result["legacy"]["traffic_alg_ratio"] = round(
                 lt["traffic_bytes"] / (result["legacy"]["alg_bytes_per_key"] * len(tables) * tables[0].n), 3)
 
+    # ---- the read shapes a Version presents, N=1:
+    # recorded beside `value` ----
+    if world == 1 and not args.no_version:
+        result["version_probe"] = version_leg(ctx, stream, dev)
+    if world == 1 and not args.no_mixed:
+        result["mixed_set"] = mixed_set_leg(ctx, stream, dev, qk, bpk)
+
     # ---- CPU baseline (host cores), rank 0 at N=1 ----
     if dist:  # every rank's share, so the N-GPU line shows each GPU's passes
         mine = gpu_share_record(rank, local, len(tables) * N, qk.n, build_bytes, probe_bytes,
@@ -698,7 +709,7 @@ def e2e_rate(ctx, stream, tables, outs, lens, fs, qk, mask, bpk, dev):
             "note": "H2D keys + build + probe + D2H filters/masks, pinned host buffers"}
 
 
-def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_500_000, reps=3):
+def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_500_000, reps=3, table_group=4):
     """Host-inclusive rate with part of the hashing on the host, as the
     reference does it (BloomHash in AddKey and in KeyMayMatch,
     full_filter_block.cc:45,271).  Keys start in pinned host memory; filters
@@ -776,16 +787,19 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
         if raw_q:
             ctx_raw.full_probe_dev(fs, dlsm_amd.Keys(d_q[: raw_q * 20], raw_q, 20), mask[: raw_q * mb])
         to_host(0, raw_t, 0, raw_q, s_raw)
-        if raw_t < T:  # the hashed tables: one batched build from their hashes
+        # the hashed tables in groups of `table_group`: each group's 4 B/key
+        # copy and batched build run while the host hashes the next group
+        for g0 in range(raw_t, T, table_group):
+            g1 = min(T, g0 + table_group)
             t0 = time.perf_counter()
-            for s_ in range(raw_t, T):
+            for s_ in range(g0, g1):
                 dlsm_amd.hash_batch(dlsm_amd.Keys(tab_np[s_], N, 20), out=hbt_np[s_ * N:(s_ + 1) * N])
             hash_s += time.perf_counter() - t0
             with torch.cuda.stream(stream):
-                dbt[raw_t * N:].copy_(hbt[raw_t * N:], non_blocking=True)
-            ctx.full_build_hashed_dev([dbt[s_ * N:(s_ + 1) * N] for s_ in range(raw_t, T)], outs[raw_t:],
-                                      lens[raw_t:], bpk)
-            to_host(raw_t, T, 0, 0, stream)
+                dbt[g0 * N:g1 * N].copy_(hbt[g0 * N:g1 * N], non_blocking=True)
+            ctx.full_build_hashed_dev([dbt[s_ * N:(s_ + 1) * N] for s_ in range(g0, g1)], outs[g0:g1],
+                                      lens[g0:g1], bpk)
+            to_host(g0, g1, 0, 0, stream)
         for lo in range(raw_q, Q, chunk_keys):
             hi = min(Q, lo + chunk_keys)
             n = hi - lo
@@ -827,7 +841,16 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
           and bool(np.array_equal(h_mask.numpy(), ref_mask)))
     ctx_raw.close()
     hashed = (T - raw_t) * N + (Q - raw_q)
+    # the host's own bound: every key's 20 bytes come out of host DRAM once
+    # (the cores read the hashed ones, the DMA engines the raw ones) and each
+    # hashed key's 4 B hash is written and read back by the DMA; against the
+    # host's streaming read rate measured now, on the same cores
+    host_bytes = 20 * K + 8 * hashed
+    host_read = host_read_rate()
     return {"mkeys_s": round(K / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
+            "host_bytes_per_step": host_bytes, "host_GBs": round(host_bytes / dt / 1e9, 2),
+            "host_read_GBs_measured": host_read["GBs"], "host_read_method": host_read["method"],
+            "frac_of_host_read": round(host_bytes / dt / 1e9 / host_read["GBs"], 4) if host_read["GBs"] else None,
             "ms_per_step_reps": [round(x * 1e3, 3) for x in times],
             "host_hashed_keys": hashed, "raw_keys": K - hashed,
             "host_hashed_tables": T - raw_t, "host_hashed_lookups": Q - raw_q,
@@ -839,6 +862,29 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
                      "first (hashed batch build), then lookups (hashed probe) -- 4 B/key H2D; the other keys "
                      "H2D as 20-byte keys on a second context and stream, hashed on the GPU; D2H filters/masks "
                      "on a third stream; pinned host buffers")}
+
+
+def host_read_rate(nbytes=2 << 30, reps=3):
+    """The host's streaming DRAM read rate on this process's cores: a parallel
+    int64 reduction (torch intra-op threads = the usable cores) over a buffer
+    far larger than the host's caches, best of `reps`.  GB/s."""
+    import torch
+
+    prev = torch.get_num_threads()
+    n = host_cores()
+    torch.set_num_threads(n)
+    try:
+        x = torch.ones(nbytes // 8, dtype=torch.int64)
+        best = 0.0
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            _ = int(x.sum())
+            dt = time.perf_counter() - t0
+            best = max(best, nbytes / dt / 1e9)
+        del x
+    finally:
+        torch.set_num_threads(prev)
+    return {"GBs": round(best, 1), "method": f"torch int64 sum over {nbytes >> 30} GiB, {n} threads, best of {reps + 1}"}
 
 
 def e2e_split(T, N, Q, hash_rate, h2d_Bps):
@@ -923,6 +969,106 @@ def cpu_baseline(args, tables, gpu_filters, qk, mask, filters, N, T, bpk, legacy
         out["sample"] += ("; util/bloom_impl.h AddHash / HashMayMatch + util/hash.cc + util/bloom.cc "
                           "compiled from the reference (full_filter_block.cc's bookkeeping restated)")
     return out
+
+
+def version_leg(ctx, stream, dev, lookups=100_000_000, reps=5, space=100_000_000):
+    """MultiGet-style probe of a version (dlsm_version_probe_dev): db_bench's
+    final version at config 5 (dlsm_amd.workload.dbbench_version: 4 level-0
+    files + 5 / 40 / 377 files on levels 1-3, 139.5 MB of filters) and
+    `lookups` Gets uniform over [0, 2 x space) -- half of them past every
+    file's range, which FindFile still sends to each level's last file
+    (db/version_set.cc:95-118).  Per lookup the files Version::Get visits
+    whose filter passes it (a u64 slot mask).  Device-resident, HIP events
+    over `reps` calls.  Algorithmic bytes: 20 B key read + 8 B mask written
+    per lookup + every filter read once.  Parity: tests/test_version_probe.py
+    (oracle) and scripts/bench_version_probe.py (first 2 M Gets)."""
+    import torch
+
+    import dlsm_amd
+    from dlsm_amd import workload as W
+
+    t0 = time.time()
+    with torch.cuda.stream(stream):  # torch's input making and the library share one stream
+        files = W.dbbench_version(ctx, dev, space)
+        ver = ctx.version(files, on_device=True)
+        filt = sum(int(f.filter.numel()) for f in files)
+        g = torch.Generator(device=dev)
+        g.manual_seed(11)
+        qv = torch.randint(0, 2 * space, (lookups,), device=dev, dtype=torch.int64, generator=g)
+        qk = dlsm_amd.Keys(W.dbbench_keys_torch(qv), lookups, 20)
+        del qv
+        mask = torch.zeros(lookups, dtype=torch.int64, device=dev)
+    snap = (1 << 56) - 1
+    ctx.version_probe_dev(ver, qk, snap, mask)  # warm
+    ctx.sync()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.version_probe_dev(ver, qk, snap, mask)
+    e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    visits = int((mask != 0).sum().item())
+    alg = lookups * (20 + 8) + filt
+    gbs = alg / (ms * 1e-3) / 1e9
+    rec = {"ms": round(ms, 4), "mgets_s": round(lookups / ms / 1e3, 1), "lookups": lookups,
+           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt,
+           "alg_bytes_per_get": round(alg / lookups, 3), "alg_GBs": round(gbs, 1),
+           "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "gets_with_a_visit": visits,
+           "note": ("roofline vs HBM streaming; the pass is bound by the random 64-byte filter-line "
+                    "reads of ~4 probes per Get (Infinity Cache / L2), not by its streamed bytes"),
+           "setup_s": round(time.time() - t0, 2)}
+    ver.close()
+    del qk, mask, files
+    return rec
+
+
+def mixed_set_leg(ctx, stream, dev, qk, bpk, reps=5):
+    """Batch probe against filters of different sizes, the shape of a
+    Version's L0 + level files (stacked per line count in groups): 8 full
+    filters of 153,846 / 153,846 / 600 K / 600 K / 1.6 M / 1.6 M / 3 M / 3 M keys
+    (filter f from v = 8i + f), the bench's lookups.  Device-resident, HIP
+    events.  Algorithmic bytes: 20 B key + 1 B mask per lookup + every filter
+    read once.  Parity: tests/test_gpu_packed_groups.py and
+    scripts/bench_probe_shapes.py (oracle)."""
+    import torch
+
+    import dlsm_amd
+    from dlsm_amd import workload as W
+
+    sizes = [153_846, 153_846, 600_000, 600_000, 1_600_000, 1_600_000, 3_000_000, 3_000_000]
+    F = len(sizes)
+    tabs, outs = [], []
+    with torch.cuda.stream(stream):  # torch's input making and the library share one stream
+        for f, n in enumerate(sizes):
+            v = torch.arange(n, device=dev, dtype=torch.int64) * F + f
+            tabs.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), n, 20))
+            outs.append(torch.zeros(dlsm_amd.full_size(n)[0], dtype=torch.uint8, device=dev))
+        lens = torch.zeros(F, dtype=torch.uint64, device=dev)
+        ctx.full_build_dev(tabs, outs, lens, bpk)
+        ctx.sync()
+        L = lens.cpu().numpy()
+        filters = [outs[f][: int(L[f])] for f in range(F)]
+        fs = ctx.filterset(filters, on_device=True)
+        mask = torch.empty(qk.n * fs.mask_bytes, dtype=torch.uint8, device=dev)
+    ctx.full_probe_dev(fs, qk, mask)  # warm
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.full_probe_dev(fs, qk, mask)
+    e1.record(stream)
+    stream.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    filt = sum(int(f.numel()) for f in filters)
+    alg = qk.n * (20 + fs.mask_bytes) + filt
+    gbs = alg / (ms * 1e-3) / 1e9
+    rec = {"ms": round(ms, 4), "mkeys_s": round(qk.n / ms / 1e3, 1), "lookups": qk.n,
+           "keys_per_filter": sizes, "filter_bytes": filt, "alg_bytes_per_key": round(alg / qk.n, 3),
+           "alg_GBs": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    fs.close()
+    del tabs, outs, filters, mask
+    return rec
 
 
 def legacy_leg(ctx, stream, tables, bpk, reps=20, direct_reps=3):

@@ -1799,12 +1799,16 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint32_t qq = lane & 3u;
-    uint4 qv[8];
+    // global (not flat) 16-byte loads, 16-byte LDS stores
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const v4u gv4u;
+    typedef __attribute__((address_space(3))) v4u lv4u;
+    v4u qv[8];
 #pragma unroll
     for (int r = 0; r < 8; r++) {
       const uint32_t t = 16u * r + (lane >> 2);
-      qv[r] = make_uint4(0u, 0u, 0u, 0u);
-      if (t < n) qv[r] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(ad[t]) + 16u * qq);
+      qv[r] = v4u{0u, 0u, 0u, 0u};
+      if (t < n) qv[r] = *(gv4u*)(ad[t] + 16u * qq);
     }
 #pragma unroll
     for (int hf = 0; hf < 2; hf++) {
@@ -1812,13 +1816,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
 #pragma unroll
       for (int r = 4 * hf; r < 4 * hf + 4; r++) {
         const uint32_t t = 16u * r + (lane >> 2);
-        if (t < n) {
-          lds32* d = st + (t - 64u * hf) * 16u + qq * 4u;
-          d[0] = qv[r].x;
-          d[1] = qv[r].y;
-          d[2] = qv[r].z;
-          d[3] = qv[r].w;
-        }
+        if (t < n) *(lv4u*)(st + (t - 64u * hf) * 16u + qq * 4u) = qv[r];
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       if (task[hf] != ~0u) {
@@ -1828,8 +1826,16 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
         const uint32_t delta = bloom_delta(hh);
         uint32_t bad = 0u;
         if constexpr (K > 0) {
+          // all K reads issued before the first use: one LDS round trip, not K
+          uint32_t w[K], sh[K];
 #pragma unroll
-          for (int q = 0; q < K; q++, hh += delta) bad |= ~line[(hh & 511u) >> 5] >> (hh & 31u);
+          for (int q = 0; q < K; q++, hh += delta) {
+            sh[q] = hh;
+            w[q] = line[(hh >> 5) & 15u];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < K; q++) bad |= ~w[q] >> (sh[q] & 31u);
         } else {
           const int kk = meta[task[hf] & 0xffffu].k;
           for (int q = 0; q < kk; q++, hh += delta) bad |= ~line[(hh & 511u) >> 5] >> (hh & 31u);
@@ -1840,7 +1846,20 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     }
   };
   const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kVRouteWaves * 64u;
-  for (uint64_t base = (static_cast<uint64_t>(blockIdx.x) * kVRouteWaves + wv) * 64u; base < kd.n; base += wstride) {
+  const uint64_t base0 = (static_cast<uint64_t>(blockIdx.x) * kVRouteWaves + wv) * 64u;
+  // K20: the next iteration's key words are loaded while this one runs (the
+  // HBM round trip of the key stream overlaps the searches and probe rounds)
+  uint32_t xn[5] = {0u, 0u, 0u, 0u, 0u};
+  auto key_words = [&](uint64_t b, uint32_t (&x)[5]) {
+    const uint64_t ii = min(b + lane, kd.n - 1);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(kd.bytes + ii * 20u);
+#pragma unroll
+    for (int j = 0; j < 5; j++) x[j] = __builtin_nontemporal_load(w + j);
+  };
+  if constexpr (MODE == KM_K20) {
+    if (base0 < kd.n) key_words(base0, xn);
+  }
+  for (uint64_t base = base0; base < kd.n; base += wstride) {
     const uint64_t i = base + lane;
     const bool live = i < kd.n;
     const uint64_t ii = live ? i : kd.n - 1;  // a dead lane reads a valid key and stores nothing
@@ -1857,10 +1876,10 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     uint32_t h;
     ulonglong2 q;
     if constexpr (MODE == KM_K20) {  // one read of the key's five words: hash and prefix
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(uk);
       uint32_t x[5];
 #pragma unroll
-      for (int j = 0; j < 5; j++) x[j] = __builtin_nontemporal_load(w + j);
+      for (int j = 0; j < 5; j++) x[j] = xn[j];
+      if (base + wstride < kd.n) key_words(base + wstride, xn);
       h = hash_init(20, kBloomSeed);
 #pragma unroll
       for (int j = 0; j < 5; j++) h = hash_word(h, x[j]);
@@ -1872,24 +1891,30 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     }
     hb[lane] = h;
     // the open interval: j = bounds below the lookup's prefix (a lower bound
-    // whose halving steps depend on nb only: the same for every lane)
+    // whose halving steps depend on nb only: the same for every lane).  A
+    // 4-ary form (three pivots per step read together, half the LDS round
+    // trips) measured 1-2 % slower: its extra compares cost more VALU than
+    // the round trips it saves (profiles/r05_version_probe_ab.txt).
+    auto below = [&](const ulonglong2& p) -> uint32_t {
+      return (p.x < q.x || (p.x == q.x && p.y < q.y)) ? 1u : 0u;
+    };
     uint32_t j = 0;
     if (nb) {
       uint32_t len = nb;
       while (len > 1) {
         const uint32_t half = len >> 1;
-        const ulonglong2 p = bnd[j + half - 1];
-        if (p.x < q.x || (p.x == q.x && p.y < q.y)) j += half;
+        if (below(bnd[j + half - 1])) j += half;
         len -= half;
       }
-      const ulonglong2 p = bnd[j];
-      if (p.x < q.x || (p.x == q.x && p.y < q.y)) j++;
+      j += below(bnd[j]);
     }
-    const bool exact = j < nb && bnd[j].x == q.x && bnd[j].y == q.y;
+    // the interval's record and the bound at j, read together (ivl has nb + 1)
+    const ulonglong2 bj = bnd[min(j, nb ? nb - 1 : 0u)];
+    const VIntervalDev R = ivl[j];
+    const bool exact = j < nb && bj.x == q.x && bj.y == q.y;
     uint64_t l0m;
     uint32_t pick[kNumLevels - 1];
     if (!exact) {
-      const VIntervalDev& R = ivl[j];
       l0m = R.l0mask;
 #pragma unroll
       for (int lv = 0; lv < kNumLevels - 1; lv++) pick[lv] = R.pick[lv];

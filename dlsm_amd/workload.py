@@ -73,3 +73,50 @@ def dbbench_keys_torch(values, key_size: int = 20):
 
 def arith_values(first: int, step: int, n: int) -> np.ndarray:
     return (np.uint64(first) + np.uint64(step) * np.arange(n, dtype=np.uint64)).astype(np.uint64)
+
+
+# The version of db_bench's final state at config 5 (the replay of DESIGN.md
+# §7: 5 + 40 + 377 files on levels 1-3 for 100 M keys, the key space spread
+# over the levels as 1 : 10 : 100) plus 4 level-0 flush files of 153,846 keys
+# over random ranges.  Level files partition [0, V); each file's filter holds
+# every key of its range on that level (stride 100 / 10 / 1).
+VERSION_SHAPE = ((1, 5, 100), (2, 40, 10), (3, 377, 1))
+
+
+def dbbench_version(ctx, dev, space: int = 100_000_000, seed: int = 11):
+    """Build the version's filters on the GPU (ctx.full_build_dev, 10 bits /
+    key) and return its dlsm_amd.VersionFile list (device filters)."""
+    import torch
+
+    from . import Keys, VersionFile, full_size
+
+    def key(v):
+        return dbbench_keys_np(np.array([v], dtype=np.uint64)).tobytes()
+
+    def build(values_dev):
+        n = int(values_dev.numel())
+        keys = Keys(dbbench_keys_torch(values_dev), n, 20)
+        out = torch.zeros(full_size(n)[0] + 16, dtype=torch.uint8, device=dev)
+        lens = torch.zeros(1, dtype=torch.uint64, device=dev)
+        ctx.full_build_dev([keys], [out], lens, 10)
+        ctx.sync()
+        return out[: int(lens.cpu()[0])].clone()
+
+    files = []
+    rng = np.random.default_rng(seed)
+    seq = 1 << 30
+    for level, nf, stride in VERSION_SHAPE:
+        edges = np.linspace(0, space, nf + 1).astype(np.int64)
+        for q in range(nf):
+            lo, hi = int(edges[q]) + (level - 1), int(edges[q + 1]) - 1
+            vals = torch.arange(lo, hi, stride, device=dev, dtype=torch.int64)
+            files.append(VersionFile(level, 10_000 * level + q, key(lo), key(int(vals[-1])), (seq << 8) | 1,
+                                     build(vals)))
+            seq -= 1
+    for j in range(4):  # level 0: flush files of 153,846 keys over random ranges
+        lo = int(rng.integers(0, space - 153_846 * 600))
+        step = int(rng.integers(50, 600))
+        vals = torch.arange(lo, lo + 153_846 * step, step, device=dev, dtype=torch.int64)
+        files.append(VersionFile(0, 900_000 + j, key(lo), key(int(vals[-1])), ((seq + 10 + j) << 8) | 1,
+                                 build(vals)))
+    return files

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--paths", default="both", choices=["both", "sliced", "direct"])
     ap.add_argument("--pass-slices", type=int, default=0, help="DLSM_OPT_VERSION_PASS_SLICES (0: default)")
     ap.add_argument("--slice-bytes", type=int, default=0, help="DLSM_OPT_VERSION_SLICE_BYTES (0: default)")
+    ap.add_argument("--no-filters", action="store_true", help="diagnostic: the same version without filters")
     args = ap.parse_args()
 
     import numpy as np
@@ -52,40 +53,15 @@ def main():
     if args.slice_bytes:
         ctx.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, args.slice_bytes)
     V = args.space
-    key = lambda v: W.dbbench_keys_np(np.array([v], dtype=np.uint64)).tobytes()  # noqa: E731
-
-    def build(values_dev):
-        n = int(values_dev.numel())
-        keys = dlsm_amd.Keys(W.dbbench_keys_torch(values_dev), n, 20)
-        out = torch.zeros(dlsm_amd.full_size(n)[0] + 16, dtype=torch.uint8, device=dev)
-        lens = torch.zeros(1, dtype=torch.uint64, device=dev)
-        ctx.full_build_dev([keys], [out], lens, 10)
-        ctx.sync()
-        return out[: int(lens.cpu()[0])].clone()
-
-    files, host_spec = [], []
+    files = W.dbbench_version(ctx, dev, V)
     rng = np.random.default_rng(11)
-    seq = 1 << 30
-    # levels 1..3: nf files partitioning [0, V), keys v = lo + stride * i
-    for level, nf, stride in ((1, 5, 100), (2, 40, 10), (3, 377, 1)):
-        edges = np.linspace(0, V, nf + 1).astype(np.int64)
-        for q in range(nf):
-            lo, hi = int(edges[q]) + (level - 1), int(edges[q + 1]) - 1
-            vals = torch.arange(lo, hi, stride, device=dev, dtype=torch.int64)
-            last = int(vals[-1])
-            files.append(VersionFile(level, 10_000 * level + q, key(lo), key(last), (seq << 8) | 1,
-                                     build(vals)))
-            host_spec.append((level, lo, last, stride))
-            seq -= 1
-    # level 0: 4 flush files of 153,846 keys over random ranges, newest last
-    for j in range(4):
-        lo = int(rng.integers(0, V - 153_846 * 600))
-        step = int(rng.integers(50, 600))
-        vals = torch.arange(lo, lo + 153_846 * step, step, device=dev, dtype=torch.int64)
-        files.append(VersionFile(0, 900_000 + j, key(lo), key(int(vals[-1])), ((seq + 10 + j) << 8) | 1,
-                                 build(vals)))
+    for _ in range(4):  # the generator state the lookups were drawn from before the shared builder
+        rng.integers(0, V - 153_846 * 600)
+        rng.integers(50, 600)
+    if args.no_filters:
+        files = [VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer, None) for f in files]
     ver = ctx.version(files, on_device=True)
-    filt_bytes = sum(int(f.filter.numel()) for f in files)
+    filt_bytes = sum(int(f.filter.numel()) for f in files if f.filter is not None)
 
     Q = args.lookups
     qv = torch.from_numpy(rng.integers(0, 2 * V, Q, dtype=np.int64)).to(dev)

@@ -131,6 +131,11 @@ def test_slice_kernels_use_no_scratch(tmp_path):
     slices = {k: v for k, v in usage.items() if "slice_kernel" in k}
     assert len(slices) >= 6, sorted(usage)
     assert all(v == 0 for v in slices.values()), slices
+    # the version probe's LDS kernel (one 1,024-thread workgroup per CU) too:
+    # a spill there would put a scratch reload on every probe round
+    vl = {k: v for k, v in usage.items() if "version_lds_kernel" in k}
+    assert len(vl) >= 8, sorted(usage)
+    assert all(v == 0 for v in vl.values()), vl
 
 
 def test_cu_subset_is_balanced_under_both_numberings():
