@@ -440,6 +440,11 @@ def main():
     # recorded beside `value` ----
     if world == 1 and not args.no_version:
         result["version_probe"] = version_leg(ctx, stream, dev)
+        vt = load_traffic(args.traffic, result["config"], "version")
+        if vt:  # fabric bytes (L2 misses, Infinity-Cache hits included) per call
+            vp = result["version_probe"]
+            vp["traffic"] = vt["traffic_bytes"]
+            vp["traffic_alg_ratio"] = round(vt["traffic_bytes"] / (vp["alg_bytes_per_get"] * vp["lookups"]), 3)
     if world == 1 and not args.no_mixed:
         result["mixed_set"] = mixed_set_leg(ctx, stream, dev, qk, bpk)
 

@@ -22,11 +22,24 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   mkdir -p "$OUT/pmc" &&
   timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e $BARGS > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-version --no-mixed $BARGS \
+    > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
 done &&
-python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" > /dev/null &&
+for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  mkdir -p "$OUT/pmcv" &&
+  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmcv/p$i" -o run -- \
+    python3 scripts/bench_version_probe.py --lookups 100000000 --check 0 --paths direct \
+    > "$OUT/pmcv/p$i.json" 2> "$OUT/pmcv/p$i.err" || exit 1
+done &&
+python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" "$OUT/pmcv" > /dev/null &&
 timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-legacy --traffic "$OUT/traffic.json" $BARGS \
-  > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
-python3 scripts/sampled_kernel_stats.py "$OUT/prof" 10 > "$OUT/sampled_kernel_stats.txt"
+  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-legacy --no-version --no-mixed \
+  --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
+python3 scripts/sampled_kernel_stats.py "$OUT/prof" 10 > "$OUT/sampled_kernel_stats.txt" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/vprof" -o run -- \
+  python3 scripts/bench_version_probe.py --lookups 100000000 --check 0 --paths direct \
+  > "$OUT/vprof.json" 2> "$OUT/vprof.err" &&
+python3 scripts/kstats.py "$OUT/vprof" > "$OUT/version_kernel_stats.txt" 2>&1 &&
+python3 scripts/shrink_outputs.py "$OUT"

@@ -8,7 +8,11 @@ so it is doubled here; WRITE_SIZE is exact for 16-B-per-lane stores.  Both
 count Infinity-Cache hits as well (memory-side counters), so the figure is
 fabric traffic, an upper bound on HBM traffic.
 
-    python scripts/pmc_traffic.py PMC_DIR BENCH_JSON OUT_JSON
+    python scripts/pmc_traffic.py PMC_DIR BENCH_JSON OUT_JSON [VERSION_PMC_DIR]
+
+VERSION_PMC_DIR: FETCH/WRITE passes of scripts/bench_version_probe.py (its
+version set-up builds 426 filters, so its launches are kept apart from the
+bench's build pass).
 """
 import csv
 import glob
@@ -20,7 +24,8 @@ from collections import defaultdict
 
 PASSES = {"probe": ("probe_partition_kernel", "probe_slice_kernel", "probe_unpermute_kernel"),
           "build": ("full_partition_kernel", "full_slice_kernel"),
-          "legacy": ("legacy_partition_kernel", "legacy_slice_kernel")}
+          "legacy": ("legacy_partition_kernel", "legacy_slice_kernel"),
+          "version": ("version_lds_kernel",)}
 
 
 def per_kernel(pmc_dir):
@@ -37,6 +42,10 @@ def main():
     pmc_dir, bench_json, out_json = sys.argv[1:4]
     bench = json.load(open(bench_json))
     vals = per_kernel(pmc_dir)
+    if len(sys.argv) > 4:  # the version probe's own passes
+        vv = per_kernel(sys.argv[4])
+        if "version_lds_kernel" in vv:
+            vals["version_lds_kernel"] = vv["version_lds_kernel"]
     out = {"source": pmc_dir, "config": {k: bench.get("config", bench).get(k) for k in
                                           ("tables", "keys_per_table", "lookups", "filters",
                                            "probe_chunk_lg", "probe_slice_lg", "keys")},
