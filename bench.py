@@ -851,7 +851,7 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     # hashed key's 4 B hash is written and read back by the DMA; against the
     # host's streaming read rate measured now, on the same cores
     host_bytes = 20 * K + 8 * hashed
-    host_read = host_read_rate()
+    host_read = host_read_rate(h_q)
     return {"mkeys_s": round(K / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
             "host_bytes_per_step": host_bytes, "host_GBs": round(host_bytes / dt / 1e9, 2),
             "host_read_GBs_measured": host_read["GBs"], "host_read_method": host_read["method"],
@@ -869,27 +869,23 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
                      "on a third stream; pinned host buffers")}
 
 
-def host_read_rate(nbytes=2 << 30, reps=3):
-    """The host's streaming DRAM read rate on this process's cores: a parallel
-    int64 reduction (torch intra-op threads = the usable cores) over a buffer
-    far larger than the host's caches, best of `reps`.  GB/s."""
-    import torch
+def host_read_rate(buf, reps=3):
+    """The host's read ceiling for the memory the host hashing reads: the
+    pinned lookup-key buffer streamed by the same pool of threads, NUMA-placed
+    the same way (dlsm_host_read_bytes: a 64-bit XOR fold, no hashing), best
+    of `reps` after one warm pass.  GB/s."""
+    import dlsm_amd
 
-    prev = torch.get_num_threads()
-    n = host_cores()
-    torch.set_num_threads(n)
-    try:
-        x = torch.ones(nbytes // 8, dtype=torch.int64)
-        best = 0.0
-        for _ in range(reps + 1):
-            t0 = time.perf_counter()
-            _ = int(x.sum())
-            dt = time.perf_counter() - t0
-            best = max(best, nbytes / dt / 1e9)
-        del x
-    finally:
-        torch.set_num_threads(prev)
-    return {"GBs": round(best, 1), "method": f"torch int64 sum over {nbytes >> 30} GiB, {n} threads, best of {reps + 1}"}
+    n = (buf.numel() * buf.element_size()) // 8 * 8
+    view = buf.view(-1)[: n // buf.element_size()] if buf.element_size() == 1 else buf
+    best = 0.0
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        dlsm_amd.host_read_bytes(view)
+        best = max(best, n / (time.perf_counter() - t0) / 1e9)
+    return {"GBs": round(best, 1),
+            "method": (f"dlsm_host_read_bytes over the {n >> 20} MiB pinned lookup-key buffer on the host-hash "
+                       f"pool ({host_cores()} threads, NUMA-placed like the hashing), best of {reps}")}
 
 
 def e2e_split(T, N, Q, hash_rate, h2d_Bps):

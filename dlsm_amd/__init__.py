@@ -118,6 +118,16 @@ def hash_batch(keys: "Keys", out: Optional[np.ndarray] = None, threads: int = 0)
     return out[: keys.n] if isinstance(out, np.ndarray) else out
 
 
+def host_read_bytes(buf, threads: int = 0) -> int:
+    """Stream a host buffer (numpy array or CPU torch tensor, size a multiple
+    of 8 bytes) on the host-hash pool, NUMA-placed like hash_batch
+    (dlsm_host_read_bytes); returns the XOR fold of its 64-bit words."""
+    n = buf.nbytes if isinstance(buf, np.ndarray) else buf.numel() * buf.element_size()
+    fold = C.c_uint64(0)
+    check(lib().dlsm_host_read_bytes(_ptr(buf), n, threads, C.byref(fold)), "host_read_bytes")
+    return int(fold.value)
+
+
 def crc32c_mask(crc: int) -> int:
     return int(lib().dlsm_crc32c_mask(crc))
 

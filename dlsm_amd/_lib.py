@@ -127,6 +127,7 @@ SIGNATURES = [
     ("dlsm_bloom_full_probe", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_full_probe_hashed_dev", C.c_int, [_VP, _VP, C.POINTER(dlsm_keyset), _VP]),
     ("dlsm_bloom_hash_batch", C.c_int, [C.POINTER(dlsm_keyset), _VP, C.c_int]),
+    ("dlsm_host_read_bytes", C.c_int, [_VP, C.c_uint64, C.c_int, C.POINTER(C.c_uint64)]),
     ("dlsm_bloom_legacy_build_dev", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _VP]),
     ("dlsm_bloom_legacy_build", C.c_int, [_VP, C.POINTER(dlsm_build_job), C.c_int, C.c_int, _U64P]),
     ("dlsm_bloom_legacy_probe_dev", C.c_int, [_VP, _VP, C.c_uint64, C.POINTER(dlsm_keyset), _VP]),

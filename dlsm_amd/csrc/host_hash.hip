@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>  // bloom_math.h's host/device qualifiers
 
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -156,9 +158,52 @@ int usable_cores() {
   return std::min(n, 64);
 }
 
+// The NUMA node holding the bytes [p, p + n): the node of three sampled pages
+// when they agree, else -1 (move_pages with no target nodes only reports).
+int numa_node_of(const void* p, uint64_t n) {
+  if (!p || n == 0) return -1;
+  const long page = sysconf(_SC_PAGESIZE);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  void* pages[3];
+  for (int i = 0; i < 3; i++)
+    pages[i] = reinterpret_cast<void*>((a + (n - 1) * static_cast<uint64_t>(i) / 2) & ~static_cast<uintptr_t>(page - 1));
+  int status[3] = {-1, -1, -1};
+  if (syscall(SYS_move_pages, 0, 3L, pages, nullptr, status, 0) != 0) return -1;
+  return status[0] >= 0 && status[0] == status[1] && status[1] == status[2] ? status[0] : -1;
+}
+
+// CPUs of NUMA node `node` that this process may use (empty if none / unknown).
+cpu_set_t node_cpus(int node, const cpu_set_t& allowed) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  char path[96];
+  std::snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return set;
+  char buf[4096] = {0};
+  const size_t len = std::fread(buf, 1, sizeof(buf) - 1, f);
+  std::fclose(f);
+  buf[len] = 0;
+  for (char* s = buf; *s;) {  // "0-63,128-191"
+    char* e = nullptr;
+    const long lo = std::strtol(s, &e, 10);
+    if (e == s) break;
+    long hi = lo;
+    if (*e == '-') hi = std::strtol(e + 1, &e, 10);
+    for (long c = lo; c <= hi && c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &allowed)) CPU_SET(c, &set);
+    s = (*e == ',') ? e + 1 : e;
+    if (*s == '\n') break;
+  }
+  return set;
+}
+
 // A process-wide fork-join pool: run(parts, f) calls f(0..parts-1) on the
 // pool's threads and the caller, returning when all are done.  One run at a
-// time (callers serialise on run_m).
+// time (callers serialise on run_m).  run(..., node): the pool's threads
+// move onto the CPUs of NUMA node `node` first (the node holding the keys:
+// hashing reads them from local DRAM instead of across the socket link; the
+// caller's own thread is left where it is), node < 0 leaves them as they are.
 class Pool {
  public:
   static Pool& get() {
@@ -166,10 +211,17 @@ class Pool {
     return p;
   }
   int size() const { return static_cast<int>(th_.size()) + 1; }
-  void run(int parts, const std::function<void(int)>& f) {
+  void run(int parts, const std::function<void(int)>& f, int node = -1) {
     std::lock_guard<std::mutex> one(run_m_);
     {
       std::lock_guard<std::mutex> lk(m_);
+      if (node != node_) {
+        node_ = node;
+        place_gen_++;
+        CPU_ZERO(&place_);
+        if (node >= 0) place_ = node_cpus(node, allowed_);
+        if (CPU_COUNT(&place_) == 0) place_ = allowed_;  // unknown node: anywhere allowed
+      }
       f_ = &f;
       parts_ = parts;
       next_.store(0);
@@ -185,6 +237,11 @@ class Pool {
 
  private:
   Pool() {
+    if (sched_getaffinity(0, sizeof(allowed_), &allowed_) != 0) {
+      CPU_ZERO(&allowed_);
+      for (int c = 0; c < CPU_SETSIZE; c++) CPU_SET(c, &allowed_);
+    }
+    place_ = allowed_;
     const int n = usable_cores() - 1;
     for (int t = 0; t < n; t++) th_.emplace_back([this] { loop(); });
   }
@@ -201,14 +258,22 @@ class Pool {
     for (int i; (i = next_.fetch_add(1)) < parts_;) (*f_)(i);
   }
   void loop() {
-    uint64_t seen = 0;
+    uint64_t seen = 0, placed = 0;
     for (;;) {
+      cpu_set_t want;
+      bool move = false;
       {
         std::unique_lock<std::mutex> lk(m_);
         cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
         if (stop_) return;
         seen = gen_;
+        if (placed != place_gen_) {
+          placed = place_gen_;
+          want = place_;
+          move = true;
+        }
       }
+      if (move) (void)sched_setaffinity(0, sizeof(want), &want);  // this thread only
       work();
       std::lock_guard<std::mutex> lk(m_);
       if (--active_ == 0) done_.notify_one();
@@ -220,8 +285,10 @@ class Pool {
   const std::function<void(int)>* f_ = nullptr;
   std::atomic<int> next_{0};
   int parts_ = 0, active_ = 0;
-  uint64_t gen_ = 0;
+  uint64_t gen_ = 0, place_gen_ = 0;
   bool stop_ = false;
+  int node_ = -1;
+  cpu_set_t allowed_, place_;
 };
 
 }  // namespace
@@ -239,10 +306,56 @@ extern "C" int dlsm_bloom_hash_batch(const dlsm_keyset* keys, uint32_t* out, int
     hash_range(ks, 0, ks.n, out);
     return DLSM_OK;
   }
+  // the pool's threads go to the NUMA node that holds the keys ($DLSM_HASH_NUMA=0: left anywhere)
+  static const bool numa = [] {
+    const char* e = getenv("DLSM_HASH_NUMA");
+    return !(e && atoi(e) == 0);
+  }();
+  const uint64_t key_bytes = ks.offsets ? ks.offsets[ks.n] : ks.n * static_cast<uint64_t>(ks.key_len);
+  const int node = numa ? numa_node_of(ks.bytes, key_bytes) : -1;
   // `width` interleaved lanes of tasks: lane t takes parts t, t + width, ...
   pool.run(width, [&](int t) {
     for (uint64_t p = static_cast<uint64_t>(t); p < parts; p += static_cast<uint64_t>(width))
       hash_range(ks, p * kPart, std::min(ks.n, (p + 1) * kPart), out);
-  });
+  }, node);
+  return DLSM_OK;
+}
+
+extern "C" int dlsm_host_read_bytes(const void* p, uint64_t n, int threads, uint64_t* fold) {
+  if (!fold || threads < 0 || (n && !p) || (n & 7u)) return DLSM_E_ARG;
+  *fold = 0;
+  if (n == 0) return DLSM_OK;
+  static const bool numa = [] {
+    const char* e = getenv("DLSM_HASH_NUMA");
+    return !(e && atoi(e) == 0);
+  }();
+  const uint64_t* w = static_cast<const uint64_t*>(p);
+  const uint64_t words = n / 8;
+  constexpr uint64_t kPart = 1u << 16;  // words per task (512 KiB)
+  const uint64_t parts = (words + kPart - 1) / kPart;
+  Pool& pool = Pool::get();
+  const int width = threads == 0 ? pool.size() : std::min(threads, pool.size());
+  std::vector<uint64_t> acc(static_cast<size_t>(width) * 8, 0);  // a cache line per lane
+  auto range = [&](uint64_t lo, uint64_t hi, uint64_t& a) {
+    uint64_t x0 = 0, x1 = 0, x2 = 0, x3 = 0;  // four chains: the loop streams, it does not wait on one xor
+    uint64_t i = lo;
+    for (; i + 4 <= hi; i += 4) {
+      x0 ^= w[i];
+      x1 ^= w[i + 1];
+      x2 ^= w[i + 2];
+      x3 ^= w[i + 3];
+    }
+    for (; i < hi; i++) x0 ^= w[i];
+    a ^= x0 ^ x1 ^ x2 ^ x3;
+  };
+  if (width <= 1 || parts == 1) {
+    range(0, words, acc[0]);
+  } else {
+    pool.run(width, [&](int t) {
+      for (uint64_t q = static_cast<uint64_t>(t); q < parts; q += static_cast<uint64_t>(width))
+        range(q * kPart, std::min(words, (q + 1) * kPart), acc[static_cast<size_t>(t) * 8]);
+    }, numa ? numa_node_of(p, n) : -1);
+  }
+  for (int t = 0; t < width; t++) *fold ^= acc[static_cast<size_t>(t) * 8];
   return DLSM_OK;
 }

@@ -388,6 +388,13 @@ int dlsm_bloom_full_probe_hashed_dev(dlsm_ctx* ctx, const dlsm_filterset* fs, co
  * dlsm_bloom_full_probe_hashed_dev.  Synchronous; no device is touched. */
 int dlsm_bloom_hash_batch(const dlsm_keyset* keys, uint32_t* out, int threads);
 
+/* Streams n host bytes at p (n a multiple of 8) on the same pool and the same
+ * NUMA placement dlsm_bloom_hash_batch uses (its threads move to the node
+ * holding the bytes), XOR-folding them into *fold: the host's read ceiling
+ * for that memory and those cores, which the host-side hashing is measured
+ * against.  Synchronous; no device is touched. */
+int dlsm_host_read_bytes(const void* p, uint64_t n, int threads, uint64_t* fold);
+
 /* ---- MultiGet-style probe of a version's files ---- */
 
 /* One SSTable of a version: its key range and its full filter.  Mirrors

@@ -162,3 +162,17 @@ def test_keys_guard_checks_data_against_host_offsets():
         dlsm_amd.Keys(np.zeros(11, dtype=np.uint8), 2, 0, offs).c()
     with pytest.raises(ValueError):
         dlsm_amd.Keys(np.zeros(12, dtype=np.uint8), 2, 0, offs[:2]).c()
+
+
+def test_host_read_bytes_folds_every_word():
+    """dlsm_host_read_bytes (the host read ceiling bench.py's e2e_hashed is
+    measured against) reads every 64-bit word once, on any thread count."""
+    import numpy as np
+
+    import dlsm_amd
+
+    x = np.random.default_rng(5).integers(0, 2**63, size=(1 << 20) + 3, dtype=np.uint64)
+    want = int(np.bitwise_xor.reduce(x))
+    for th in (0, 1, 3):
+        assert dlsm_amd.host_read_bytes(x, th) == want
+    assert dlsm_amd.host_read_bytes(x[:0]) == 0

@@ -103,6 +103,19 @@ def test_two_logical_devices_strong_scaling_parity(orc):
         assert dt > 0 and len(passes) == 2 and all(len(p) == 2 for p in passes)
         assert all(b > 0 and p > 0 for d in passes for b, p in d)
         assert len(dev_s) == 2 and all(0 < x <= dt * 1.001 for x in dev_s)
+        # the older entry points time device 0's passes only: the
+        # other devices keep their overlapped steps; pass_ms holds device 0's
+        import ctypes as C
+
+        from dlsm_amd import _lib as L
+        from dlsm_amd import check, lib
+
+        arr = (L.dlsm_device_work * 2)(*[w.device_work() for w in workers])
+        for fn, every in (("dlsm_multi_device_run", None), ("dlsm_multi_device_run_sampled", 1)):
+            wall, pm = C.c_double(0.0), (C.c_float * 4)(-2, -2, -2, -2)
+            args = (arr, 2, 10, 2, 1) + ((every,) if every else ()) + (C.byref(wall), pm)
+            check(getattr(lib(), fn)(*args), fn)
+            assert wall.value > 0 and all(x > 0 for x in pm), (fn, list(pm))
         assert [w.work.tables for w in workers] == [list(range(0, 16, 2)), list(range(1, 16, 2))]
         assert [(w.work.lookup_lo, w.work.lookup_hi) for w in workers] == [(0, _Q // 2), (_Q // 2, _Q)]
         union = {}
