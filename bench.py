@@ -869,7 +869,7 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
                      "on a third stream; pinned host buffers")}
 
 
-def host_read_rate(buf, reps=3):
+def host_read_rate(buf, reps=5):
     """The host's read ceiling for the memory the host hashing reads: the
     pinned lookup-key buffer streamed by the same pool of threads, NUMA-placed
     the same way (dlsm_host_read_bytes: a 64-bit XOR fold, no hashing), best
