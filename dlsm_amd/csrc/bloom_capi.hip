@@ -2080,10 +2080,15 @@ namespace {
 // version (139.5 MB of filters) takes 4.0 ms direct against 5.4 ms with its
 // two big levels sliced (profiles/r05_version_probe.txt).
 // ($DLSM_VERSION_SLICE_MIN_BYTES overrides; 0 disables the sliced probe.)
+// The sliced version probe measured slower than the direct one at both level
+// sizes tried (db_bench's 125 MB level 3: 3.76 vs 3.48 ms per 100 M Gets; a
+// 1.25 GB level 3: 11.1 vs 5.0 ms; profiles/r05_p_version_large.txt), so no
+// level is sliced unless a caller asks ($DLSM_VERSION_SLICE_MIN_BYTES or
+// DLSM_OPT_VERSION_SLICE_BYTES: levels whose filters exceed that many bytes).
 uint64_t version_slice_min_bytes() {
   static const uint64_t v = [] {
     const char* e = getenv("DLSM_VERSION_SLICE_MIN_BYTES");
-    return e ? strtoull(e, nullptr, 10) : (uint64_t(256) << 20);
+    return e ? strtoull(e, nullptr, 10) : uint64_t(0);
   }();
   return v;
 }

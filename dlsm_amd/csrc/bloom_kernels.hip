@@ -1808,6 +1808,8 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     for (int r = 0; r < 8; r++) {
       const uint32_t t = 16u * r + (lane >> 2);
       qv[r] = v4u{0u, 0u, 0u, 0u};
+      // default cache policy: the level-0 / level-1 lines are L2 hits (with
+      // the non-temporal hint they miss: 2.1 x slower, r05_p_version_line_nt_ab.txt)
       if (t < n) qv[r] = *(gv4u*)(ad[t] + 16u * qq);
     }
 #pragma unroll

@@ -193,10 +193,12 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             before touching the device; 0 (default) off
  *   DLSM_OPT_VERSION_SLICE_BYTES  dlsm_version_create on this context: a level >= 1 whose
  *                             filters hold more bytes goes to the sliced version probe
- *                             (0: default 256 MiB or $DLSM_VERSION_SLICE_MIN_BYTES;
- *                             UINT64_MAX: never)
+ *                             (0: $DLSM_VERSION_SLICE_MIN_BYTES, default never --
+ *                             the sliced probe measured slower at 125 MB and 1.25 GB
+ *                             levels; UINT64_MAX: never)
  *   DLSM_OPT_VERSION_PASS_SLICES  128 KiB slices per partition pass of the sliced version
- *                             probe, 1..1024 (default 1024; larger levels take several) */
+ *                             probe, 1..1024 (default 1024; larger levels take several)
+ */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
 #define DLSM_OPT_BUILD_GROUPS 2

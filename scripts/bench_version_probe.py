@@ -32,7 +32,9 @@ def main():
     ap.add_argument("--check", type=int, default=200_000, help="lookups checked against the oracle")
     ap.add_argument("--paths", default="both", choices=["both", "sliced", "direct"])
     ap.add_argument("--pass-slices", type=int, default=0, help="DLSM_OPT_VERSION_PASS_SLICES (0: default)")
-    ap.add_argument("--slice-bytes", type=int, default=0, help="DLSM_OPT_VERSION_SLICE_BYTES (0: default)")
+    ap.add_argument("--slice-bytes", type=int, default=64 << 20,
+                    help="DLSM_OPT_VERSION_SLICE_BYTES for the version (levels whose filters exceed it are "
+                         "sliced; the library's default slices none): path 0 probes them sliced, path 1 direct")
     ap.add_argument("--no-filters", action="store_true", help="diagnostic: the same version without filters")
     args = ap.parse_args()
 
@@ -50,8 +52,9 @@ def main():
     ctx.set_stream(stream)
     if args.pass_slices:
         ctx.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, args.pass_slices)
-    if args.slice_bytes:
+    if args.slice_bytes and args.paths != "direct":
         ctx.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, args.slice_bytes)
+    res_slice = args.slice_bytes if args.paths != "direct" else None
     V = args.space
     files = W.dbbench_version(ctx, dev, V)
     rng = np.random.default_rng(11)
@@ -69,7 +72,8 @@ def main():
     mask = torch.zeros(Q, dtype=torch.int64, device=dev)
     snap = (1 << 56) - 1
     res = {"what": "version probe (batched Get over a version), device-resident",
-           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt_bytes, "lookups": Q}
+           "files_per_level": [4, 5, 40, 377, 0, 0], "filter_bytes": filt_bytes, "lookups": Q,
+           "slice_bytes": res_slice}
     want = None
     if args.check:
         import oracle
@@ -81,9 +85,12 @@ def main():
         hq = qk.data[: n * 20].cpu().numpy()
         want, _ = oracle.version_probe(hf, hq, n, snapshot=snap)
         res["oracle_checked"] = n
-    # path 0: levels whose filters outgrow an XCD's L2 take the sliced probe
-    # (route / partition / LDS slice / unpermute); path 1: every level direct
-    for path, label in ((0, "sliced"), (1, "direct")):
+    # path 0: levels past --slice-bytes take the sliced probe (route /
+    # partition / LDS slice / unpermute); path 1: every level direct.  With
+    # both, the two alternate twice (the first timed run of a process can
+    # run slow) and each keeps its faster run.
+    order = [(0, "sliced"), (1, "direct")] * (2 if args.paths == "both" else 1)
+    for path, label in order:
         if args.paths != "both" and args.paths != label:
             continue
         ctx.set_path(path)
@@ -100,7 +107,10 @@ def main():
         if want is not None:
             got = mask[: res["oracle_checked"]].cpu().numpy().astype(np.uint64)
             rec["matches_oracle"] = bool(np.array_equal(got, np.asarray(want, dtype=np.uint64)))
-        res[label] = rec
+        if label not in res or rec["ms"] < res[label]["ms"]:
+            if label in res and "matches_oracle" in res[label]:
+                rec["matches_oracle"] = rec.get("matches_oracle", True) and res[label]["matches_oracle"]
+            res[label] = rec
     ctx.set_path(0)
     print(json.dumps(res), flush=True)
 
