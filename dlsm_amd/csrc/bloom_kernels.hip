@@ -1736,9 +1736,11 @@ constexpr int kVQueue = kVRound + 64;     // queued probe tasks per wave (one en
 constexpr size_t kVWaveLds = 64 * 64 + kVRound * 8 + kVQueue * 4 + 64 * 4 + 64 * 8;
 constexpr size_t kVLdsMax = 160u * 1024u;  // the CU's LDS
 
-size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf) {
-  return static_cast<size_t>(n_bnd) * 16u + (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev) +
-         static_cast<size_t>(nf) * sizeof(VMeta) + kVRouteWaves * kVWaveLds;
+size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf, int gt) {  // gt: version_lds_kernel's GT
+  size_t tables = 0;
+  if (gt <= 1) tables += static_cast<size_t>(n_bnd) * 16u;
+  if (gt == 0) tables += (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev) + static_cast<size_t>(nf) * sizeof(VMeta);
+  return tables + kVRouteWaves * kVWaveLds;
 }
 
 // FullFilterBlockReader::KeyMayMatch (full_filter_block.cc:269-284) for one
@@ -1748,7 +1750,13 @@ __device__ __forceinline__ uint32_t full_may_match_all(uint32_t h, const VMeta& 
   return full_may_match(h, g);
 }
 
-template <int MODE, bool ROUTE, int K>
+// GT: where the version's tables live.  0: all in LDS (up to ~450 files
+// beside the wave queues); 1: the bound prefixes in LDS (the search's chain of
+// dependent reads; up to ~1,800 files), the interval records and the file
+// metadata read from global memory (L2-resident, one read per lookup / per
+// probe task); 2: all in global memory.  The probes go through the wave
+// queues either way.
+template <int MODE, bool ROUTE, int K, int GT>
 __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
                                                                 uint64_t* __restrict__ slot_mask,
                                                                 uint32_t* __restrict__ level_file,
@@ -1756,12 +1764,36 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
                                                                 uint32_t nf) {
   extern __shared__ uint4 vdyn[];
   const uint32_t nb = v.n_bnd;
-  ulonglong2* bnd = reinterpret_cast<ulonglong2*>(vdyn);
-  VIntervalDev* ivl = reinterpret_cast<VIntervalDev*>(bnd + nb);
-  VMeta* meta = reinterpret_cast<VMeta*>(ivl + nb + 1);
+  ulonglong2* lbnd = reinterpret_cast<ulonglong2*>(vdyn);
+  VIntervalDev* livl = reinterpret_cast<VIntervalDev*>(lbnd + nb);
+  VMeta* lmeta = reinterpret_cast<VMeta*>(livl + nb + 1);
+  const ulonglong2* bnd;
+  const VIntervalDev* ivl;
+  uint8_t* wbase;
+  if constexpr (GT == 2) {
+    bnd = v.bnd;
+    ivl = v.ivl;
+    wbase = reinterpret_cast<uint8_t*>(vdyn);
+  } else if constexpr (GT == 1) {
+    bnd = lbnd;
+    ivl = v.ivl;
+    wbase = reinterpret_cast<uint8_t*>(lbnd + nb);
+  } else {
+    bnd = lbnd;
+    ivl = livl;
+    wbase = reinterpret_cast<uint8_t*>(lmeta + nf);
+  }
+  auto meta_at = [&](uint32_t f) -> VMeta {
+    if constexpr (GT != 0) {
+      const VFileDev& F = v.files[f];
+      return VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
+    } else {
+      return lmeta[f];
+    }
+  };
   const uint32_t lane = threadIdx.x & 63u;
   const int wv = wave_id();
-  uint8_t* wl = reinterpret_cast<uint8_t*>(meta + nf) + static_cast<size_t>(wv) * kVWaveLds;
+  uint8_t* wl = wbase + static_cast<size_t>(wv) * kVWaveLds;
   typedef __attribute__((address_space(3))) uint32_t lds32;
   typedef __attribute__((address_space(3))) unsigned long long lds64;
   lds32* st = (lds32*)reinterpret_cast<uint32_t*>(wl);                                // 64 lines of 64 B
@@ -1769,11 +1801,14 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   lds32* tq = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8);
   lds32* hb = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8 + kVQueue * 4);
   lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVRound * 8 + kVQueue * 4 + 64 * 4);
-  for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) bnd[f] = v.bnd[f];
-  for (uint32_t f = threadIdx.x; f <= nb; f += kVRouteNT) ivl[f] = v.ivl[f];
-  for (uint32_t f = threadIdx.x; f < nf; f += kVRouteNT) {
-    const VFileDev& F = v.files[f];
-    meta[f] = VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
+  if constexpr (GT != 2)
+    for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) lbnd[f] = v.bnd[f];
+  if constexpr (GT == 0) {
+    for (uint32_t f = threadIdx.x; f <= nb; f += kVRouteNT) livl[f] = v.ivl[f];
+    for (uint32_t f = threadIdx.x; f < nf; f += kVRouteNT) {
+      const VFileDev& F = v.files[f];
+      lmeta[f] = VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
+    }
   }
   mb[lane] = 0ull;
   __syncthreads();
@@ -1792,7 +1827,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       task[hf] = t < n ? tq[t] : ~0u;
       h[hf] = 0u;
       if (task[hf] != ~0u) {
-        const VMeta& F = meta[task[hf] & 0xffffu];
+        const VMeta F = meta_at(task[hf] & 0xffffu);
         h[hf] = hb[task[hf] >> 26];
         ad[t] = reinterpret_cast<unsigned long long>(F.data + (fastmod(h[hf], F.L, F.magic) << 6));
       }
@@ -1839,7 +1874,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
 #pragma unroll
           for (int q = 0; q < K; q++) bad |= ~w[q] >> (sh[q] & 31u);
         } else {
-          const int kk = meta[task[hf] & 0xffffu].k;
+          const int kk = meta_at(task[hf] & 0xffffu).k;
           for (int q = 0; q < kk; q++, hh += delta) bad |= ~line[(hh & 511u) >> 5] >> (hh & 31u);
         }
         if (!(bad & 1u)) atomicOr((unsigned long long*)&mb[task[hf] >> 26], 1ull << ((task[hf] >> 16) & 63u));
@@ -1978,7 +2013,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     const uint64_t anyl0 = uniform64(__ballot(l0m != 0));
     for (uint32_t f = 0; anyl0 && f < v.n_l0; f++) {  // level 0: newest first
       const bool in = (l0m >> f) & 1u;
-      const VMeta& F = meta[f];
+      const VMeta F = meta_at(f);
       if (in && F.data == nullptr) m |= 1ull << f;
       if (in && F.data != nullptr && F.lg != 6 && full_may_match_all(h, F)) m |= 1ull << f;  // rare: 1-byte lines
       enqueue(in && F.data != nullptr && F.lg == 6, f, f);
@@ -1989,7 +2024,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       uint32_t gline = kVNoLine;
       bool task = false;
       if (pf != 0xffffffffu) {
-        const VMeta& F = meta[pf];
+        const VMeta F = meta_at(pf);
         if (ROUTE && v.lvl_sliced[lv] >= 0 && F.data != nullptr) {
           gline = F.line0 + fastmod(h, F.L, F.magic);
         } else if (F.data == nullptr) {
@@ -2947,28 +2982,41 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
   const bool route = hv != nullptr;
   uint32_t nf = v.n_l0;
   for (int lv = 1; lv < kNumLevels; lv++) nf = std::max(nf, v.lvl_begin[lv] + v.lvl_count[lv]);
-  // $DLSM_VERSION_LDS=0: the global-table kernel (A/B)
-  static const bool lds_ok = [] {
+  // $DLSM_VERSION_LDS (A/B): 0 the lane-per-lookup kernel; 2 / 3 the
+  // wave-queued kernel with GT >= 1 / GT = 2 even when the tables fit
+  static const int lds_mode = [] {
     const char* e = getenv("DLSM_VERSION_LDS");
-    return !(e && atoi(e) == 0);
+    return e ? atoi(e) : 1;
   }();
-  const size_t lds = version_lds_bytes(v.n_bnd, nf);
-  if (lds_ok && lds <= kVLdsMax) {
+  int gt = lds_mode == 3 ? 2 : (lds_mode == 2 ? 1 : 0);
+  while (gt < 2 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
+  const size_t lds = version_lds_bytes(v.n_bnd, nf, gt);
+  if (lds_mode != 0 && lds <= kVLdsMax) {
     // all files probed directly or through the queue share one probe count
     // in the common case (one bits_per_key): k = 6 unrolled
     bool k6 = true;
     (void)k6;
     const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((keys.n + kVRouteNT - 1) / kVRouteNT,
                                                                 static_cast<uint64_t>(device_cus())));
-#define DLSM_VLDS(MM, RR, KK)                                                                                   \
+#define DLSM_VLDS_GT(MM, RR, KK, GG)                                                                            \
   do {                                                                                                          \
     static bool attr = false;                                                                                   \
     if (!attr) {                                                                                                \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&version_lds_kernel<MM, RR, KK>),                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&version_lds_kernel<MM, RR, KK, GG>),             \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kVLdsMax));       \
       attr = true;                                                                                              \
     }                                                                                                           \
-    version_lds_kernel<MM, RR, KK><<<g, kVRouteNT, lds, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl, nf); \
+    version_lds_kernel<MM, RR, KK, GG><<<g, kVRouteNT, lds, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl, \
+                                                                 nf);                                           \
+  } while (0)
+#define DLSM_VLDS(MM, RR, KK)                 \
+  do {                                        \
+    if (gt == 0)                              \
+      DLSM_VLDS_GT(MM, RR, KK, 0);            \
+    else if (gt == 1)                         \
+      DLSM_VLDS_GT(MM, RR, KK, 1);            \
+    else                                      \
+      DLSM_VLDS_GT(MM, RR, KK, 2);            \
   } while (0)
     if (v.k_all == 6) {
       if (k20 && route) DLSM_VLDS(KM_K20, true, 6);
@@ -2982,6 +3030,7 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
       else DLSM_VLDS(KM_GENERIC, false, 0);
     }
 #undef DLSM_VLDS
+#undef DLSM_VLDS_GT
     return hipGetLastError();
   }
   const unsigned g = static_cast<unsigned>((keys.n + kBlock - 1) / kBlock);

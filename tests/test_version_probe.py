@@ -285,3 +285,54 @@ def test_gpu_version_probe_sliced_internal_var_keys(gpu):
     finally:
         gpu.set_option(dlsm_amd.OPT_VERSION_SLICE_BYTES, old)
         gpu.set_option(dlsm_amd.OPT_VERSION_PASS_SLICES, 1024)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l1_files", [900, 2400])
+def test_gpu_version_probe_many_files(gpu, l1_files):
+    """Versions whose tables do not all fit the LDS beside the wave queues:
+    4 + 900 + 60 files (the bound prefixes in LDS, interval records and file
+    metadata from global memory) and 4 + 2,400 + 60 (everything from global
+    memory).  Slot masks and picked files equal the oracle's, for 20-byte
+    keys and for 28-byte internal keys."""
+    import torch
+
+    import dlsm_amd
+
+    rng = np.random.default_rng(9)
+    span = 3_000_000
+    files = []
+    for j in range(4):
+        a = int(rng.integers(0, span // 2))
+        vals = np.arange(a, a + 400_000, 97 + j)
+        files.append(VersionFile(0, 9000 + j, K(vals[0]), K(vals[-1]), (((1 << 40) + j) << 8) | 1,
+                                 build_filter(vals)))
+    for level, nf, step in ((1, l1_files, 29), (2, 60, 13)):
+        edges = np.linspace(0, span, nf + 1).astype(np.int64)
+        for q in range(nf):
+            vals = np.arange(edges[q] + q % 5, edges[q + 1] - 1, step)
+            files.append(VersionFile(level, 1000 * level + q, K(vals[0]), K(vals[-1]),
+                                     (int(rng.integers(1, 1 << 40)) << 8) | 1, build_filter(vals)))
+    n = 300_000
+    v_ = np.concatenate([rng.integers(0, span + span // 10, n - 3), [0, span - 1, 5 * span]]).astype(np.uint64)
+    q = oracle.keys_from_values(v_)
+    snap = (1 << 56) - 1
+    want, want_lf = oracle.version_probe(files, q, n, snapshot=snap)
+    v = gpu.version(files)
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    # the same lookups as 28-byte internal keys (K28 key mode)
+    ik = np.concatenate([q.reshape(n, 20), np.frombuffer(((5 << 8) | 1).to_bytes(8, "little") * n,
+                                                         dtype=np.uint8).reshape(n, 8)], axis=1).reshape(-1)
+    want28, _ = oracle.version_probe(files, ik, n, snapshot=snap, stride=28, suffix=8)
+    assert np.array_equal(want28, want)  # the trailer never changes a user-key comparison
+    mask.zero_()
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(np.ascontiguousarray(ik)).cuda(), n, 28, suffix_len=8),
+                          snap, mask)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want28)
+    v.close()
