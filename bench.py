@@ -445,6 +445,10 @@ def main():
             vp = result["version_probe"]
             vp["traffic"] = vt["traffic_bytes"]
             vp["traffic_alg_ratio"] = round(vt["traffic_bytes"] / (vp["alg_bytes_per_get"] * vp["lookups"]), 3)
+            # the bytes the kernel does move (filter lines past L2 dominate) per
+            # second, against the same 8 TB/s: what bounds it, unlike `frac`
+            vp["traffic_GBs"] = round(vt["traffic_bytes"] / (vp["ms"] * 1e-3) / 1e9, 1)
+            vp["traffic_frac"] = round(vp["traffic_GBs"] / HBM_PEAK_GBS, 4)
     if world == 1 and not args.no_mixed:
         result["mixed_set"] = mixed_set_leg(ctx, stream, dev, qk, bpk)
 
