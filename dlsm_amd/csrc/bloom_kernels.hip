@@ -1739,7 +1739,8 @@ constexpr size_t kVLdsMax = 160u * 1024u;  // the CU's LDS
 size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf, int gt) {  // gt: version_lds_kernel's GT
   size_t tables = 0;
   if (gt <= 1) tables += static_cast<size_t>(n_bnd) * 16u;
-  if (gt == 0) tables += (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev) + static_cast<size_t>(nf) * sizeof(VMeta);
+  if (gt <= 2) tables += static_cast<size_t>(nf) * sizeof(VMeta);
+  if (gt == 0) tables += (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev);
   return tables + kVRouteWaves * kVWaveLds;
 }
 
@@ -1750,12 +1751,15 @@ __device__ __forceinline__ uint32_t full_may_match_all(uint32_t h, const VMeta& 
   return full_may_match(h, g);
 }
 
-// GT: where the version's tables live.  0: all in LDS (up to ~450 files
-// beside the wave queues); 1: the bound prefixes in LDS (the search's chain of
-// dependent reads; up to ~1,800 files), the interval records and the file
-// metadata read from global memory (L2-resident, one read per lookup / per
-// probe task); 2: all in global memory.  The probes go through the wave
-// queues either way.
+// GT: how much of the version's tables the LDS holds, in the order they
+// matter (measured: profiles/r05_t, r05_u_version_table_tiers.txt): the file
+// metadata (read per probe task, inside every round's chain), the bound
+// prefixes (the search's chain of dependent reads), the interval records
+// (one read per lookup).  0: all three (up to ~450 files beside the wave
+// queues); 1: the metadata and the prefixes (~900 files); 2: the metadata
+// (~1,800 files); 3: none.  What the LDS does not hold is read from global
+// memory, where it stays in L2.  The probes go through the wave queues
+// either way.
 template <int MODE, bool ROUTE, int K, int GT>
 __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
                                                                 uint64_t* __restrict__ slot_mask,
@@ -1764,31 +1768,23 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
                                                                 uint32_t nf) {
   extern __shared__ uint4 vdyn[];
   const uint32_t nb = v.n_bnd;
+  constexpr bool kMeta = GT <= 2, kBnd = GT <= 1, kIvl = GT == 0;
   ulonglong2* lbnd = reinterpret_cast<ulonglong2*>(vdyn);
-  VIntervalDev* livl = reinterpret_cast<VIntervalDev*>(lbnd + nb);
-  VMeta* lmeta = reinterpret_cast<VMeta*>(livl + nb + 1);
+  VMeta* lmeta = reinterpret_cast<VMeta*>(lbnd + (kBnd ? nb : 0u));
+  VIntervalDev* livl = reinterpret_cast<VIntervalDev*>(lmeta + (kMeta ? nf : 0u));
+  uint8_t* wbase = reinterpret_cast<uint8_t*>(livl + (kIvl ? nb + 1u : 0u));
   const ulonglong2* bnd;
   const VIntervalDev* ivl;
-  uint8_t* wbase;
-  if constexpr (GT == 2) {
-    bnd = v.bnd;
-    ivl = v.ivl;
-    wbase = reinterpret_cast<uint8_t*>(vdyn);
-  } else if constexpr (GT == 1) {
-    bnd = lbnd;
-    ivl = v.ivl;
-    wbase = reinterpret_cast<uint8_t*>(lbnd + nb);
-  } else {
-    bnd = lbnd;
-    ivl = livl;
-    wbase = reinterpret_cast<uint8_t*>(lmeta + nf);
-  }
+  if constexpr (kBnd) bnd = lbnd;
+  else bnd = v.bnd;
+  if constexpr (kIvl) ivl = livl;
+  else ivl = v.ivl;
   auto meta_at = [&](uint32_t f) -> VMeta {
-    if constexpr (GT != 0) {
+    if constexpr (kMeta) {
+      return lmeta[f];
+    } else {
       const VFileDev& F = v.files[f];
       return VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
-    } else {
-      return lmeta[f];
     }
   };
   const uint32_t lane = threadIdx.x & 63u;
@@ -1801,15 +1797,15 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   lds32* tq = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8);
   lds32* hb = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8 + kVQueue * 4);
   lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVRound * 8 + kVQueue * 4 + 64 * 4);
-  if constexpr (GT != 2)
+  if constexpr (kBnd)
     for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) lbnd[f] = v.bnd[f];
-  if constexpr (GT == 0) {
-    for (uint32_t f = threadIdx.x; f <= nb; f += kVRouteNT) livl[f] = v.ivl[f];
+  if constexpr (kMeta)
     for (uint32_t f = threadIdx.x; f < nf; f += kVRouteNT) {
       const VFileDev& F = v.files[f];
       lmeta[f] = VMeta{F.f.data, F.f.L, F.f.magic, F.line0, F.f.k, F.f.lg, 0u};
     }
-  }
+  if constexpr (kIvl)
+    for (uint32_t f = threadIdx.x; f <= nb; f += kVRouteNT) livl[f] = v.ivl[f];
   mb[lane] = 0ull;
   __syncthreads();
   const uint64_t tnum = (snapshot << 8) | 1u;  // LookupKey(user_key, snapshot): kValueTypeForSeek
@@ -2982,14 +2978,14 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
   const bool route = hv != nullptr;
   uint32_t nf = v.n_l0;
   for (int lv = 1; lv < kNumLevels; lv++) nf = std::max(nf, v.lvl_begin[lv] + v.lvl_count[lv]);
-  // $DLSM_VERSION_LDS (A/B): 0 the lane-per-lookup kernel; 2 / 3 the
-  // wave-queued kernel with GT >= 1 / GT = 2 even when the tables fit
+  // $DLSM_VERSION_LDS (A/B): 0 the lane-per-lookup kernel; 2 / 3 / 4 the
+  // wave-queued kernel with GT >= 1 / 2 / 3 even when more tables fit
   static const int lds_mode = [] {
     const char* e = getenv("DLSM_VERSION_LDS");
     return e ? atoi(e) : 1;
   }();
-  int gt = lds_mode == 3 ? 2 : (lds_mode == 2 ? 1 : 0);
-  while (gt < 2 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
+  int gt = lds_mode >= 2 ? std::min(lds_mode, 4) - 1 : 0;
+  while (gt < 3 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
   const size_t lds = version_lds_bytes(v.n_bnd, nf, gt);
   if (lds_mode != 0 && lds <= kVLdsMax) {
     // all files probed directly or through the queue share one probe count
@@ -3015,8 +3011,10 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
       DLSM_VLDS_GT(MM, RR, KK, 0);            \
     else if (gt == 1)                         \
       DLSM_VLDS_GT(MM, RR, KK, 1);            \
-    else                                      \
+    else if (gt == 2)                         \
       DLSM_VLDS_GT(MM, RR, KK, 2);            \
+    else                                      \
+      DLSM_VLDS_GT(MM, RR, KK, 3);            \
   } while (0)
     if (v.k_all == 6) {
       if (k20 && route) DLSM_VLDS(KM_K20, true, 6);
