@@ -1880,17 +1880,33 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   };
   const uint64_t wstride = static_cast<uint64_t>(gridDim.x) * kVRouteWaves * 64u;
   const uint64_t base0 = (static_cast<uint64_t>(blockIdx.x) * kVRouteWaves + wv) * 64u;
-  // K20: the next iteration's key words are loaded while this one runs (the
-  // HBM round trip of the key stream overlaps the searches and probe rounds)
+  // K20: the next iteration's key words are loaded at the top of this one
+  // and digested (hash, prefix) at its bottom, so the HBM round trip of the
+  // key stream overlaps the searches and probe rounds, and what crosses the
+  // loop's back edge is the digest, not the loaded registers (a loaded
+  // register carried across it makes the compiler copy it -- and wait for
+  // the load -- right where it is issued)
   uint32_t xn[5] = {0u, 0u, 0u, 0u, 0u};
+  uint32_t hn = 0u;
+  ulonglong2 qn = make_ulonglong2(0ull, 0ull);
   auto key_words = [&](uint64_t b, uint32_t (&x)[5]) {
     const uint64_t ii = min(b + lane, kd.n - 1);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(kd.bytes + ii * 20u);
 #pragma unroll
     for (int j = 0; j < 5; j++) x[j] = __builtin_nontemporal_load(w + j);
   };
+  auto digest = [&](const uint32_t (&x)[5]) {  // one read of the key's five words: hash and prefix
+    hn = hash_init(20, kBloomSeed);
+#pragma unroll
+    for (int j = 0; j < 5; j++) hn = hash_word(hn, x[j]);
+    qn.x = (static_cast<uint64_t>(__builtin_bswap32(x[0])) << 32) | __builtin_bswap32(x[1]);
+    qn.y = (static_cast<uint64_t>(__builtin_bswap32(x[2])) << 32) | __builtin_bswap32(x[3]);
+  };
   if constexpr (MODE == KM_K20) {
-    if (base0 < kd.n) key_words(base0, xn);
+    if (base0 < kd.n) {
+      key_words(base0, xn);
+      digest(xn);
+    }
   }
   for (uint64_t base = base0; base < kd.n; base += wstride) {
     const uint64_t i = base + lane;
@@ -1908,16 +1924,10 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     const uint8_t* uk = kd.bytes + s;
     uint32_t h;
     ulonglong2 q;
-    if constexpr (MODE == KM_K20) {  // one read of the key's five words: hash and prefix
-      uint32_t x[5];
-#pragma unroll
-      for (int j = 0; j < 5; j++) x[j] = xn[j];
+    if constexpr (MODE == KM_K20) {
+      h = hn;
+      q = qn;
       if (base + wstride < kd.n) key_words(base + wstride, xn);
-      h = hash_init(20, kBloomSeed);
-#pragma unroll
-      for (int j = 0; j < 5; j++) h = hash_word(h, x[j]);
-      q.x = (static_cast<uint64_t>(__builtin_bswap32(x[0])) << 32) | __builtin_bswap32(x[1]);
-      q.y = (static_cast<uint64_t>(__builtin_bswap32(x[2])) << 32) | __builtin_bswap32(x[3]);
     } else {
       h = key_hash<MODE>(kd, ii);
       q = key_prefix<MODE>(uk, l);
@@ -2042,6 +2052,9 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     if (live) {
       slot_mask[i] = m;
       if (ROUTE) hv[i] = h;
+    }
+    if constexpr (MODE == KM_K20) {
+      if (base + wstride < kd.n) digest(xn);
     }
   }
 }

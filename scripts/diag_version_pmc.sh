@@ -8,8 +8,8 @@ V=${2:-}
 mkdir -p "$OUT"
 i=0
 # $VPMC_GROUPS: counter groups separated by ';' (default: fabric bytes and L2 hits)
-IFS=';' read -r -a GROUPS <<< "${VPMC_GROUPS:-FETCH_SIZE;TCC_HIT_sum TCC_MISS_sum;TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum}"
-for grp in "${GROUPS[@]}"; do
+IFS=';' read -r -a CGRPS <<< "${VPMC_GROUPS:-FETCH_SIZE;TCC_HIT_sum TCC_MISS_sum;TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum}"
+for grp in "${CGRPS[@]}"; do
   for lib in new $V; do
     i=$((i + 1))
     if [ "$lib" = new ]; then unset DLSM_LIB_VARIANT; else export DLSM_LIB_VARIANT=$lib; fi
