@@ -3000,7 +3000,9 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
   int gt = lds_mode >= 2 ? std::min(lds_mode, 4) - 1 : 0;
   while (gt < 3 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
   const size_t lds = version_lds_bytes(v.n_bnd, nf, gt);
-  if (lds_mode != 0 && lds <= kVLdsMax) {
+  // a queued probe task names its file in 16 bits: larger versions take the
+  // lane-per-lookup kernel
+  if (lds_mode != 0 && lds <= kVLdsMax && nf <= 0xffffu) {
     // all files probed directly or through the queue share one probe count
     // in the common case (one bits_per_key): k = 6 unrolled
     bool k6 = true;

@@ -639,14 +639,23 @@ int orc_version_probe(const orc_version_file* files, int n_files, const uint8_t*
                       uint64_t snapshot, uint64_t* out_mask, uint32_t* out_level_file) {
   enum { kNumLevels = 6 };
   int l0[64], n_l0 = 0;
-  int lvl[kNumLevels][4096];
+  int* lvl[kNumLevels] = {0};  /* Version::files_[level], any size */
   int nlvl[kNumLevels] = {0};
+  for (int level = 1; level < kNumLevels; level++) {
+    lvl[level] = (int*)malloc(sizeof(int) * (size_t)(n_files > 0 ? n_files : 1));
+    if (!lvl[level]) {
+      for (int b = 1; b < level; b++) free(lvl[b]);
+      return ORC_E_ARG;
+    }
+  }
   for (int f = 0; f < n_files; f++) {
     if (files[f].level == 0) {
-      if (n_l0 == 64) return ORC_E_ARG;
+      if (n_l0 == 64) {
+        for (int b = 1; b < kNumLevels; b++) free(lvl[b]);
+        return ORC_E_ARG;
+      }
       l0[n_l0++] = f;
     } else {
-      if (nlvl[files[f].level] == 4096) return ORC_E_ARG;
       lvl[files[f].level][nlvl[files[f].level]++] = f;
     }
   }
@@ -697,6 +706,7 @@ int orc_version_probe(const orc_version_file* files, int n_files, const uint8_t*
     }
     out_mask[i] = m;
   }
+  for (int level = 1; level < kNumLevels; level++) free(lvl[level]);
   return 0;
 }
 

@@ -336,3 +336,31 @@ def test_gpu_version_probe_many_files(gpu, l1_files):
     gpu.sync()
     assert np.array_equal(mask.cpu().numpy().view(np.uint64), want28)
     v.close()
+
+
+@pytest.mark.gpu
+def test_gpu_version_probe_more_files_than_task_bits(gpu):
+    """More than 65,535 files: a queued probe task names its file in 16 bits,
+    so such a version takes the lane-per-lookup kernel; its answers equal the
+    oracle's like every other version's."""
+    import torch
+
+    import dlsm_amd
+
+    nf = 70_000
+    files = [VersionFile(1, 10 + q, K(10 * q), K(10 * q + 5), ((q + 1) << 8) | 1,
+                         build_filter(np.array([10 * q, 10 * q + 3]))) for q in range(nf)]
+    files.append(VersionFile(0, 5, K(0), K(10 * nf), (1 << 40 << 8) | 1, build_filter(np.arange(0, 10 * nf, 7))))
+    n = 200_000
+    v_ = np.random.default_rng(3).integers(0, 10 * nf + 100, n).astype(np.uint64)
+    q = oracle.keys_from_values(v_)
+    snap = (1 << 56) - 1
+    want, want_lf = oracle.version_probe(files, q, n, snapshot=snap)
+    v = gpu.version(files)
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    v.close()
