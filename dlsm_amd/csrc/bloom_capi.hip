@@ -2180,17 +2180,17 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
   for (uint32_t j = 0; j <= n_bnd; j++) {
     VIntervalDev& r = ivl[j];
     r.l0mask = 0;
-    r.reserved = 0;
+    r.reserved[0] = r.reserved[1] = r.reserved[2] = 0;
     for (int f = 0; f < n_l0; f++)  // smallest <= lookup <= largest
       if (is[f] < j && il[f] >= j) r.l0mask |= 1ull << f;
     for (int lv = 1; lv < kNumLevels; lv++) {
-      r.pick[lv - 1] = 0xffffffffu;
-      if (!count[lv]) continue;
+      r.pick[lv - 1] = 0xffffu;
+      if (!count[lv] || begin[lv] + count[lv] > 0xffffu) continue;  // (> 65,535 files: never read)
       // FindFile (version_set.cc:95-118): files [0, count-1) whose largest
       // sorts below the lookup come first; right starts at count-1
       uint32_t right = 0;
       while (right < count[lv] - 1 && il[begin[lv] + right] < j) right++;
-      if (is[begin[lv] + right] < j) r.pick[lv - 1] = begin[lv] + right;
+      if (is[begin[lv] + right] < j) r.pick[lv - 1] = static_cast<uint16_t>(begin[lv] + right);
     }
   }
   const uint64_t bnd_bytes = (sizeof(ulonglong2) * std::max<size_t>(1, bnd.size()) + 255) & ~uint64_t(255);

@@ -87,9 +87,10 @@ constexpr uint32_t kVPlanBudget = 512;                         // slice-pass wor
 // whose prefix equals a bound takes the full comparison path.
 struct VIntervalDev {
   uint64_t l0mask;                  // bit f: level-0 file f (search order) holds the lookup
-  uint32_t pick[kNumLevels - 1];    // per level 1..5: the picked file (search order index) or ~0u
-  uint32_t reserved;
+  uint16_t pick[kNumLevels - 1];    // per level 1..5: the picked file (search order index) or 0xffff
+  uint16_t reserved[3];             // (24 B: the wave-queued kernel, the only reader, takes <= 65,535 files)
 };
+static_assert(sizeof(VIntervalDev) == 24, "interval record layout");
 
 // Files in search order: level-0 newest first, then levels 1.. in key order.
 struct VersionDev {

@@ -1731,9 +1731,9 @@ constexpr int kVRouteNT = 1024;           // 16 waves, one workgroup per CU (the
 constexpr int kVRouteWaves = kVRouteNT / 64;
 constexpr int kVRound = 128;              // tasks per round: two 64-line halves' loads in flight
 constexpr int kVQueue = kVRound + 64;     // queued probe tasks per wave (one enqueue adds <= 64)
-// per wave: staged task lines (one half) | task line addresses | task queue |
-// owning lanes' hashes | their answer masks
-constexpr size_t kVWaveLds = 64 * 64 + kVRound * 8 + kVQueue * 4 + 64 * 4 + 64 * 8;
+// per wave: staged task lines (one half) | queued tasks' line addresses |
+// queued task words | owning lanes' hashes | their answer masks
+constexpr size_t kVWaveLds = 64 * 64 + kVQueue * 8 + kVQueue * 4 + 64 * 4 + 64 * 8;
 constexpr size_t kVLdsMax = 160u * 1024u;  // the CU's LDS
 
 size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf, int gt) {  // gt: version_lds_kernel's GT
@@ -1741,7 +1741,7 @@ size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf, int gt) {  // gt: version_
   if (gt <= 1) tables += static_cast<size_t>(n_bnd) * 16u;
   if (gt <= 2) tables += static_cast<size_t>(nf) * sizeof(VMeta);
   if (gt == 0) tables += (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev);
-  return tables + kVRouteWaves * kVWaveLds;
+  return ((tables + 63u) & ~static_cast<size_t>(63u)) + kVRouteWaves * kVWaveLds;
 }
 
 // FullFilterBlockReader::KeyMayMatch (full_filter_block.cc:269-284) for one
@@ -1772,7 +1772,11 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   ulonglong2* lbnd = reinterpret_cast<ulonglong2*>(vdyn);
   VMeta* lmeta = reinterpret_cast<VMeta*>(lbnd + (kBnd ? nb : 0u));
   VIntervalDev* livl = reinterpret_cast<VIntervalDev*>(lmeta + (kMeta ? nf : 0u));
-  uint8_t* wbase = reinterpret_cast<uint8_t*>(livl + (kIvl ? nb + 1u : 0u));
+  // the wave areas start 64-byte aligned (ds_write_b128 staging; the 24-byte
+  // interval records leave the tables' end 8-byte aligned only)
+  uint8_t* wbase = reinterpret_cast<uint8_t*>(vdyn) +
+                   ((reinterpret_cast<uint8_t*>(livl + (kIvl ? nb + 1u : 0u)) - reinterpret_cast<uint8_t*>(vdyn) + 63u) &
+                    ~static_cast<size_t>(63u));
   const ulonglong2* bnd;
   const VIntervalDev* ivl;
   if constexpr (kBnd) bnd = lbnd;
@@ -1793,10 +1797,10 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   typedef __attribute__((address_space(3))) uint32_t lds32;
   typedef __attribute__((address_space(3))) unsigned long long lds64;
   lds32* st = (lds32*)reinterpret_cast<uint32_t*>(wl);                                // 64 lines of 64 B
-  lds64* ad = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096);              // kVRound line addresses
-  lds32* tq = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8);
-  lds32* hb = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVRound * 8 + kVQueue * 4);
-  lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVRound * 8 + kVQueue * 4 + 64 * 4);
+  lds64* ad = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096);              // kVQueue line addresses
+  lds32* tq = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVQueue * 8);
+  lds32* hb = (lds32*)reinterpret_cast<uint32_t*>(wl + 4096 + kVQueue * 8 + kVQueue * 4);
+  lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVQueue * 8 + kVQueue * 4 + 64 * 4);
   if constexpr (kBnd)
     for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) lbnd[f] = v.bnd[f];
   if constexpr (kMeta)
@@ -1809,11 +1813,11 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   mb[lane] = 0ull;
   __syncthreads();
   const uint64_t tnum = (snapshot << 8) | 1u;  // LookupKey(user_key, snapshot): kValueTypeForSeek
-  // One round: tasks tq[0, n), n <= kVRound, wave-uniform.  Lane t computes
-  // the line addresses of tasks t and t + 64; every line is fetched four lanes
-  // per line (lane & 3 = its 16-byte quarter), both halves' loads in flight
-  // at once; each half is staged in LDS in turn and lane t tests its task's
-  // k bits there.
+  // One round: tasks tq[0, n), n <= kVRound, wave-uniform, their line
+  // addresses in ad[0, n) (written by the lane that queued each task).  Every
+  // line is fetched four lanes per line (lane & 3 = its 16-byte quarter),
+  // both halves' loads in flight at once; each half is staged in LDS in turn
+  // and lane t tests task t + 64 hf's k bits there.
   auto round = [&](uint32_t n) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     uint32_t task[2], h[2];
@@ -1821,14 +1825,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     for (int hf = 0; hf < 2; hf++) {
       const uint32_t t = lane + 64u * hf;
       task[hf] = t < n ? tq[t] : ~0u;
-      h[hf] = 0u;
-      if (task[hf] != ~0u) {
-        const VMeta F = meta_at(task[hf] & 0xffffu);
-        h[hf] = hb[task[hf] >> 26];
-        ad[t] = reinterpret_cast<unsigned long long>(F.data + (fastmod(h[hf], F.L, F.magic) << 6));
-      }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const uint32_t qq = lane & 3u;
     // global (not flat) 16-byte loads, 16-byte LDS stores
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -1843,6 +1840,9 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       // the non-temporal hint they miss: 2.1 x slower, r05_p_version_line_nt_ab.txt)
       if (t < n) qv[r] = *(gv4u*)(ad[t] + 16u * qq);
     }
+    // the owning lanes' hashes, read while the lines are in flight
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++) h[hf] = task[hf] != ~0u ? hb[task[hf] >> 26] : 0u;
 #pragma unroll
     for (int hf = 0; hf < 2; hf++) {
       if (64u * hf >= n) break;  // wave-uniform
@@ -1960,7 +1960,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     if (!exact) {
       l0m = R.l0mask;
 #pragma unroll
-      for (int lv = 0; lv < kNumLevels - 1; lv++) pick[lv] = R.pick[lv];
+      for (int lv = 0; lv < kNumLevels - 1; lv++) pick[lv] = R.pick[lv] == 0xffffu ? 0xffffffffu : R.pick[lv];
     } else {
       // the full comparisons (version_probe_kernel's), tables in global memory
       auto vs_small = [&](uint32_t f) {
@@ -1998,21 +1998,29 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
     uint32_t queued = 0;  // wave-uniform
     // a direct probe of file f for slot `slot` (this lane, if `want`): queued;
     // a full queue answers a round of 64
-    auto enqueue = [&](bool want, uint32_t f, uint32_t slot) {
+    // the queueing lane writes its task's line address too (it holds the
+    // file's metadata and its hash): a round reads the addresses in one LDS
+    // round trip instead of three
+    auto enqueue = [&](bool want, uint32_t f, uint32_t slot, const VMeta& F) {
       const uint64_t b = __ballot(want);
       if (!b) return;
       if (want) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(b >> 32),
                                                          __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(b), 0u));
         tq[queued + below] = (lane << 26) | (slot << 16) | f;
+        ad[queued + below] = reinterpret_cast<unsigned long long>(F.data + (fastmod(h, F.L, F.magic) << 6));
       }
       queued += static_cast<uint32_t>(__builtin_popcountll(b));
       if (queued >= static_cast<uint32_t>(kVRound)) {
         round(kVRound);
         const uint32_t rest = queued - kVRound;  // move the overflow (< 64) to the front
         const uint32_t t = lane < rest ? tq[kVRound + lane] : 0u;
+        const unsigned long long a = lane < rest ? ad[kVRound + lane] : 0ull;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        if (lane < rest) tq[lane] = t;
+        if (lane < rest) {
+          tq[lane] = t;
+          ad[lane] = a;
+        }
         queued = rest;
       }
     };
@@ -2022,15 +2030,16 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       const VMeta F = meta_at(f);
       if (in && F.data == nullptr) m |= 1ull << f;
       if (in && F.data != nullptr && F.lg != 6 && full_may_match_all(h, F)) m |= 1ull << f;  // rare: 1-byte lines
-      enqueue(in && F.data != nullptr && F.lg == 6, f, f);
+      enqueue(in && F.data != nullptr && F.lg == 6, f, f, F);
     }
     for (int lv = 1; lv < kNumLevels; lv++) {
       const uint32_t slot = v.n_l0 + lv - 1;
       const uint32_t pf = live && v.lvl_count[lv] ? pick[lv - 1] : 0xffffffffu;
       uint32_t gline = kVNoLine;
       bool task = false;
+      VMeta F{};
       if (pf != 0xffffffffu) {
-        const VMeta F = meta_at(pf);
+        F = meta_at(pf);
         if (ROUTE && v.lvl_sliced[lv] >= 0 && F.data != nullptr) {
           gline = F.line0 + fastmod(h, F.L, F.magic);
         } else if (F.data == nullptr) {
@@ -2041,7 +2050,7 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
           task = true;
         }
       }
-      enqueue(task, pf, slot);
+      enqueue(task, pf, slot, F);
       if (live && level_file)
         level_file[i * (kNumLevels - 1) + (lv - 1)] = pf == 0xffffffffu ? pf : pf - v.lvl_begin[lv];
       if (ROUTE && live && v.lvl_sliced[lv] >= 0) gl[static_cast<uint64_t>(v.lvl_sliced[lv]) * kd.n + i] = gline;
