@@ -1755,9 +1755,9 @@ __device__ __forceinline__ uint32_t full_may_match_all(uint32_t h, const VMeta& 
 // matter (measured: profiles/r05_t, r05_u_version_table_tiers.txt): the file
 // metadata (read per probe task, inside every round's chain), the bound
 // prefixes (the search's chain of dependent reads), the interval records
-// (one read per lookup).  0: all three (up to ~450 files beside the wave
-// queues); 1: the metadata and the prefixes (~900 files); 2: the metadata
-// (~1,800 files); 3: none.  What the LDS does not hold is read from global
+// (one read per lookup).  0: all three (up to ~440 files beside the wave
+// queues); 1: the metadata and the prefixes (~770 files); 2: the metadata
+// (~1,500 files); 3: none.  What the LDS does not hold is read from global
 // memory, where it stays in L2.  The probes go through the wave queues
 // either way.
 template <int MODE, bool ROUTE, int K, int GT>

@@ -291,8 +291,8 @@ def test_gpu_version_probe_sliced_internal_var_keys(gpu):
 @pytest.mark.parametrize("l1_files", [600, 900, 2400])
 def test_gpu_version_probe_many_files(gpu, l1_files):
     """Versions whose tables do not all fit the LDS beside the wave queues:
-    4 + 600 + 60 files (bound prefixes and file metadata in LDS, interval
-    records from global memory), 4 + 900 + 60 (the prefixes alone in LDS) and
+    4 + 600 + 60 files (file metadata and bound prefixes in LDS, interval
+    records from global memory), 4 + 900 + 60 (the metadata alone in LDS) and
     4 + 2,400 + 60 (everything from global memory).  Slot masks and picked
     files equal the oracle's, for 20-byte keys and for 28-byte internal keys."""
     import torch
