@@ -364,3 +364,92 @@ def test_gpu_version_probe_more_files_than_task_bits(gpu):
     assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
     assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
     v.close()
+
+
+def random_version(rng, n_l0, span):
+    """A version of random shape: n_l0 overlapping level-0 files, levels 1-5
+    with 0-80 range-partitioned files each (some levels empty), filters of
+    bits_per_key 2-20 (k 1-13; the kernels' k = 6 specialisation and the
+    generic loop), a fifth of the files without a filter, one-key files."""
+    files = []
+    num = 1
+    for j in range(n_l0):
+        a = int(rng.integers(0, span))
+        b = min(span, a + int(rng.integers(1, span // 2)))
+        vals = np.unique(rng.integers(a, b + 1, int(rng.integers(1, 3000))))
+        filt = None if rng.random() < 0.2 else build_filter_bpk(vals, int(rng.integers(2, 21)))
+        files.append(VersionFile(0, num, K(vals[0]), K(vals[-1]), (int(rng.integers(1, 1 << 50)) << 8) | 1, filt))
+        num += 1
+    for level in range(1, 6):
+        nf = int(rng.integers(0, 81)) if rng.random() < 0.85 else 0
+        if nf == 0:
+            continue
+        edges = np.sort(rng.choice(np.arange(1, span), size=2 * nf, replace=False))
+        for q in range(nf):
+            lo, hi = int(edges[2 * q]), int(edges[2 * q + 1])
+            vals = np.unique(rng.integers(lo, hi + 1, int(rng.integers(1, 2000))))
+            vals = np.unique(np.concatenate([[lo, hi], vals]))  # the file's bounds are keys of the file
+            filt = None if rng.random() < 0.2 else build_filter_bpk(vals, int(rng.integers(2, 21)))
+            files.append(VersionFile(level, num, K(lo), K(hi), (int(rng.integers(1, 1 << 50)) << 8) | 1, filt))
+            num += 1
+    return files
+
+
+def build_filter_bpk(values, bpk):
+    keys = oracle.keys_from_values(np.asarray(values, dtype=np.uint64))
+    return oracle.full_build(keys, len(values), bpk=bpk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_gpu_version_probe_random_shapes(gpu, seed):
+    """Random versions (level-0 counts 0-50, levels of 0-80 files, empty levels,
+    filters of k 1-13 and none, one-key files) against lookups that are half
+    keys of the files (filters pass: long probe queues) and half uniform, at
+    random snapshots: slot masks and picked files equal the oracle's, for
+    20-byte keys and as 28-byte internal keys."""
+    import torch
+
+    import dlsm_amd
+
+    rng = np.random.default_rng(100 + seed)
+    span = 2_000_000
+    n_l0 = [0, 1, 7, 23, 50, 12, 3, 40][seed]
+    files = random_version(rng, n_l0, span)
+    n = 150_001
+    hits = rng.integers(0, span + 1, n // 2)
+    v_ = np.concatenate([hits, rng.integers(0, span + span // 5, n - n // 2)]).astype(np.uint64)
+    q = oracle.keys_from_values(v_)
+    snap = int(rng.integers(1, 1 << 52))
+    want, want_lf = oracle.version_probe(files, q, n, snapshot=snap)
+    v = gpu.version(files)
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    ik = np.concatenate([q.reshape(n, 20), np.frombuffer(((snap & 0xffff) << 8 | 1).to_bytes(8, "little") * n,
+                                                         dtype=np.uint8).reshape(n, 8)], axis=1).reshape(-1)
+    want28, _ = oracle.version_probe(files, ik, n, snapshot=snap, stride=28, suffix=8)
+    mask.zero_()
+    gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(np.ascontiguousarray(ik)).cuda(), n, 28, suffix_len=8),
+                          snap, mask)
+    gpu.sync()
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want28)
+    v.close()
+
+
+def test_oracle_random_shapes_consistent():
+    """CPU check of the random-shape generator and the oracle: the filter only
+    removes candidates, and every lookup that is a key of a file with a filter
+    keeps that file when it is the file Version::Get visits."""
+    rng = np.random.default_rng(7)
+    files = random_version(rng, 9, 200_000)
+    n = 20_000
+    q = oracle.keys_from_values(rng.integers(0, 220_000, n).astype(np.uint64))
+    mask, lf = oracle.version_probe(files, q, n, snapshot=1 << 51)
+    nofilt = [VersionFile(f.level, f.number, f.smallest, f.largest, f.largest_trailer, None) for f in files]
+    cand, lf2 = oracle.version_probe(nofilt, q, n, snapshot=1 << 51)
+    assert np.array_equal(lf, lf2)
+    assert np.all((mask & ~cand) == 0) and cand.any()
