@@ -650,3 +650,46 @@ def test_crc32c_dev_vs_oracle(gpu, golden, orc):
         bufs.append(t[1:] if n > 100 else t)  # also an unaligned start
         want.append(orc.crc32c((b[1:] if n > 100 else b).tobytes()))
     assert gpu.crc32c_dev(bufs) == want
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_full_probe_random_sets(gpu, orc, seed):
+    """Random filter sets: 1-24 filters of 0-400 K keys each at bits_per_key
+    2-20 (some sets of equal line counts, some mixed: stacked, packed and
+    grouped images, direct groups), lookups of a random count and key length
+    (16 / 20 / 28 / 33 bytes), half of them keys of the filters.  Every path
+    (auto, direct, sliced where the set allows it) equals the oracle."""
+    import dlsm_amd
+
+    rng = np.random.default_rng(500 + seed)
+    F = int(rng.integers(1, 25))
+    key_len = [20, 28, 16, 33, 20, 28][seed]
+    equal = seed % 2 == 0
+    n_eq = int(rng.integers(1, 400_000))
+    tabs, ns = [], []
+    for f in range(F):
+        n = n_eq if equal else int(rng.integers(0, 400_000))
+        vals = rng.integers(0, 1 << 40, n).astype(np.uint64)
+        tabs.append(vals)
+        ns.append(n)
+    bpk = int(rng.integers(2, 21)) if equal else None
+    filters = [orc.full_build(orc.keys_from_values(t, key_len), n, stride=key_len,
+                              bpk=bpk or int(rng.integers(2, 21))) for t, n in zip(tabs, ns)]
+    nq = int(rng.integers(1, 700_000))
+    pool = np.concatenate([t for t in tabs if t.size] + [np.zeros(1, np.uint64)])
+    vals = np.where(rng.random(nq) < 0.5, pool[rng.integers(0, pool.size, nq)],
+                    rng.integers(0, 1 << 40, nq).astype(np.uint64)).astype(np.uint64)
+    q = orc.keys_from_values(vals, key_len)
+    want = orc.full_probe(filters, q, nq, stride=key_len, nthreads=8)
+    fs = gpu.filterset(filters)
+    for path in PATHS:
+        gpu.set_path(path)
+        try:
+            got = gpu.full_probe(fs, dlsm_amd.Keys(q, nq, key_len))
+        except dlsm_amd.DlsmError:
+            assert path == 2  # a set with an unsliceable group refuses the forced sliced path
+            continue
+        finally:
+            gpu.set_path(0)
+        assert np.array_equal(got, want), (path, F, key_len, equal)
+    fs.close()
