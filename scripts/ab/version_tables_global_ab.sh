@@ -1,7 +1,7 @@
 # Version probe (db_bench shape, direct, 100 M Gets) by how much of its tables
-# the LDS holds (DLSM_VERSION_LDS=1: all, the default up to ~450 files; =2:
-# bound prefixes + file metadata, the tier up to ~900 files; =3: the prefixes,
-# up to ~1,800; =4: none), interleaved on one box.
+# the LDS holds (DLSM_VERSION_LDS=1: all, the default up to ~440 files; =2:
+# file metadata + bound prefixes, the tier up to ~770 files; =3: the
+# metadata, up to ~1,500; =4: none), interleaved on one box.
 set -e
 for r in 1 2; do
   for m in 1 2 3 4; do
