@@ -1736,11 +1736,14 @@ constexpr int kVQueue = kVRound + 64;     // queued probe tasks per wave (one en
 constexpr size_t kVWaveLds = 64 * 64 + kVQueue * 8 + kVQueue * 4 + 64 * 4 + 64 * 8;
 constexpr size_t kVLdsMax = 160u * 1024u;  // the CU's LDS
 
+constexpr uint32_t kVSparse = 8;  // bounds per global window of the sparse bound index (128 B)
+
 size_t version_lds_bytes(uint32_t n_bnd, uint32_t nf, int gt) {  // gt: version_lds_kernel's GT
   size_t tables = 0;
   if (gt <= 1) tables += static_cast<size_t>(n_bnd) * 16u;
   if (gt <= 2) tables += static_cast<size_t>(nf) * sizeof(VMeta);
   if (gt == 0) tables += (static_cast<size_t>(n_bnd) + 1u) * sizeof(VIntervalDev);
+  if (gt == 2 || gt == 3) tables += static_cast<size_t>((n_bnd + kVSparse - 1) / kVSparse) * 16u;
   return ((tables + 63u) & ~static_cast<size_t>(63u)) + kVRouteWaves * kVWaveLds;
 }
 
@@ -1757,9 +1760,12 @@ __device__ __forceinline__ uint32_t full_may_match_all(uint32_t h, const VMeta& 
 // prefixes (the search's chain of dependent reads), the interval records
 // (one read per lookup).  0: all three (up to ~440 files beside the wave
 // queues); 1: the metadata and the prefixes (~770 files); 2: the metadata
-// (~1,500 files); 3: none.  What the LDS does not hold is read from global
-// memory, where it stays in L2.  The probes go through the wave queues
-// either way.
+// and every kVSparse-th prefix (~1,350 files); 3: every kVSparse-th prefix
+// (~12,000 files); 4: none.  What the LDS does not hold is read from
+// global memory, where it stays in L2; with the sparse prefixes the search
+// ends in one window of kVSparse global prefixes read together (one L2
+// round trip instead of a chain of log2(n_bnd)).  The probes go through the
+// wave queues either way.
 template <int MODE, bool ROUTE, int K, int GT>
 __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, KeyDesc kd, uint64_t snapshot,
                                                                 uint64_t* __restrict__ slot_mask,
@@ -1768,9 +1774,11 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
                                                                 uint32_t nf) {
   extern __shared__ uint4 vdyn[];
   const uint32_t nb = v.n_bnd;
-  constexpr bool kMeta = GT <= 2, kBnd = GT <= 1, kIvl = GT == 0;
+  constexpr bool kMeta = GT <= 2, kBnd = GT <= 1, kIvl = GT == 0, kSp = GT == 2 || GT == 3;
+  const uint32_t nsp = kSp ? (nb + kVSparse - 1) / kVSparse : 0u;  // sparse prefixes
   ulonglong2* lbnd = reinterpret_cast<ulonglong2*>(vdyn);
-  VMeta* lmeta = reinterpret_cast<VMeta*>(lbnd + (kBnd ? nb : 0u));
+  ulonglong2* lsp = lbnd + (kBnd ? nb : 0u);
+  VMeta* lmeta = reinterpret_cast<VMeta*>(lsp + nsp);
   VIntervalDev* livl = reinterpret_cast<VIntervalDev*>(lmeta + (kMeta ? nf : 0u));
   // the wave areas start 64-byte aligned (ds_write_b128 staging; the 24-byte
   // interval records leave the tables' end 8-byte aligned only)
@@ -1803,6 +1811,8 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
   lds64* mb = (lds64*)reinterpret_cast<unsigned long long*>(wl + 4096 + kVQueue * 8 + kVQueue * 4 + 64 * 4);
   if constexpr (kBnd)
     for (uint32_t f = threadIdx.x; f < nb; f += kVRouteNT) lbnd[f] = v.bnd[f];
+  if constexpr (kSp)  // window w's last prefix (the table's last for a short last window)
+    for (uint32_t w = threadIdx.x; w < nsp; w += kVRouteNT) lsp[w] = v.bnd[min(w * kVSparse + kVSparse - 1u, nb - 1u)];
   if constexpr (kMeta)
     for (uint32_t f = threadIdx.x; f < nf; f += kVRouteNT) {
       const VFileDev& F = v.files[f];
@@ -1942,7 +1952,36 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       return (p.x < q.x || (p.x == q.x && p.y < q.y)) ? 1u : 0u;
     };
     uint32_t j = 0;
-    if (nb) {
+    if constexpr (kSp) {
+      // the sparse prefixes in LDS pick the window (windows whose last prefix
+      // is below q), then the window's kVSparse prefixes, read together from
+      // global memory, are counted: window c's last prefix is not below q, so
+      // j lies inside it (a clamped read repeats the table's last prefix,
+      // which is not below q either)
+      uint32_t c = 0;
+      if (nsp) {
+        uint32_t len = nsp;
+        while (len > 1) {
+          const uint32_t half = len >> 1;
+          if (below(lsp[c + half - 1])) c += half;
+          len -= half;
+        }
+        c += below(lsp[c]);
+      }
+      if (c >= nsp) {
+        j = nb;
+      } else {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(1))) const u64x2 gu2;  // global, not flat, loads
+        const gu2* gb = (const gu2*)v.bnd;
+        u64x2 win[kVSparse];
+#pragma unroll
+        for (uint32_t k = 0; k < kVSparse; k++) win[k] = gb[min(c * kVSparse + k, nb - 1u)];
+        j = c * kVSparse;
+#pragma unroll
+        for (uint32_t k = 0; k < kVSparse; k++) j += below(make_ulonglong2(win[k].x, win[k].y));
+      }
+    } else if (nb) {
       uint32_t len = nb;
       while (len > 1) {
         const uint32_t half = len >> 1;
@@ -3000,22 +3039,20 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
   const bool route = hv != nullptr;
   uint32_t nf = v.n_l0;
   for (int lv = 1; lv < kNumLevels; lv++) nf = std::max(nf, v.lvl_begin[lv] + v.lvl_count[lv]);
-  // $DLSM_VERSION_LDS (A/B): 0 the lane-per-lookup kernel; 2 / 3 / 4 the
-  // wave-queued kernel with GT >= 1 / 2 / 3 even when more tables fit
+  // $DLSM_VERSION_LDS (A/B): 0 the lane-per-lookup kernel; 2 / 3 / 4 / 5 the
+  // wave-queued kernel with GT >= 1 / 2 / 3 / 4 even when more tables fit
   static const int lds_mode = [] {
     const char* e = getenv("DLSM_VERSION_LDS");
     return e ? atoi(e) : 1;
   }();
-  int gt = lds_mode >= 2 ? std::min(lds_mode, 4) - 1 : 0;
-  while (gt < 3 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
+  int gt = lds_mode >= 2 ? std::min(lds_mode, 5) - 1 : 0;
+  while (gt < 4 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
   const size_t lds = version_lds_bytes(v.n_bnd, nf, gt);
   // a queued probe task names its file in 16 bits: larger versions take the
   // lane-per-lookup kernel
   if (lds_mode != 0 && lds <= kVLdsMax && nf <= 0xffffu) {
     // all files probed directly or through the queue share one probe count
     // in the common case (one bits_per_key): k = 6 unrolled
-    bool k6 = true;
-    (void)k6;
     const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((keys.n + kVRouteNT - 1) / kVRouteNT,
                                                                 static_cast<uint64_t>(device_cus())));
 #define DLSM_VLDS_GT(MM, RR, KK, GG)                                                                            \
@@ -3037,8 +3074,10 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
       DLSM_VLDS_GT(MM, RR, KK, 1);            \
     else if (gt == 2)                         \
       DLSM_VLDS_GT(MM, RR, KK, 2);            \
-    else                                      \
+    else if (gt == 3)                         \
       DLSM_VLDS_GT(MM, RR, KK, 3);            \
+    else                                      \
+      DLSM_VLDS_GT(MM, RR, KK, 4);            \
   } while (0)
     if (v.k_all == 6) {
       if (k20 && route) DLSM_VLDS(KM_K20, true, 6);

@@ -292,8 +292,8 @@ def test_gpu_version_probe_sliced_internal_var_keys(gpu):
 def test_gpu_version_probe_many_files(gpu, l1_files):
     """Versions whose tables do not all fit the LDS beside the wave queues:
     4 + 600 + 60 files (file metadata and bound prefixes in LDS, interval
-    records from global memory), 4 + 900 + 60 (the metadata alone in LDS) and
-    4 + 2,400 + 60 (everything from global memory).  Slot masks and picked
+    records from global memory), 4 + 900 + 60 (the metadata and the sparse
+    bound index in LDS) and 4 + 2,400 + 60 (the sparse bound index alone).  Slot masks and picked
     files equal the oracle's, for 20-byte keys and for 28-byte internal keys."""
     import torch
 
@@ -339,15 +339,17 @@ def test_gpu_version_probe_many_files(gpu, l1_files):
 
 
 @pytest.mark.gpu
-def test_gpu_version_probe_more_files_than_task_bits(gpu):
-    """More than 65,535 files: a queued probe task names its file in 16 bits,
-    so such a version takes the lane-per-lookup kernel; its answers equal the
-    oracle's like every other version's."""
+@pytest.mark.parametrize("nf", [5_000, 20_000, 70_000])
+def test_gpu_version_probe_more_files_than_task_bits(gpu, nf):
+    """Versions past the LDS tables: 5,001 files keep only the sparse bound
+    index in LDS (windows of 8 prefixes read from global memory), 20,001 keep
+    nothing there, and more than 65,535 files -- a queued probe task names its
+    file in 16 bits -- take the lane-per-lookup kernel; their answers equal
+    the oracle's like every other version's."""
     import torch
 
     import dlsm_amd
 
-    nf = 70_000
     files = [VersionFile(1, 10 + q, K(10 * q), K(10 * q + 5), ((q + 1) << 8) | 1,
                          build_filter(np.array([10 * q, 10 * q + 3]))) for q in range(nf)]
     files.append(VersionFile(0, 5, K(0), K(10 * nf), (1 << 40 << 8) | 1, build_filter(np.arange(0, 10 * nf, 7))))
@@ -361,8 +363,8 @@ def test_gpu_version_probe_more_files_than_task_bits(gpu):
     lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
     gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
     gpu.sync()
-    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want)
-    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), want), nf
+    assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf), nf
     v.close()
 
 
