@@ -2071,6 +2071,17 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       if (in && F.data != nullptr && F.lg != 6 && full_may_match_all(h, F)) m |= 1ull << f;  // rare: 1-byte lines
       enqueue(in && F.data != nullptr && F.lg == 6, f, f, F);
     }
+    // metadata in global memory: every level's pick read up front, the loads
+    // in flight together (inside the loop each would wait behind the
+    // previous level's enqueue)
+    VMeta FP[kNumLevels - 1];
+    if constexpr (!kMeta) {
+#pragma unroll
+      for (int lv = 1; lv < kNumLevels; lv++) {
+        const uint32_t pf = live && v.lvl_count[lv] ? pick[lv - 1] : 0xffffffffu;
+        FP[lv - 1] = pf != 0xffffffffu ? meta_at(pf) : VMeta{};
+      }
+    }
     for (int lv = 1; lv < kNumLevels; lv++) {
       const uint32_t slot = v.n_l0 + lv - 1;
       const uint32_t pf = live && v.lvl_count[lv] ? pick[lv - 1] : 0xffffffffu;
@@ -2078,7 +2089,8 @@ __global__ __launch_bounds__(kVRouteNT) void version_lds_kernel(VersionDev v, Ke
       bool task = false;
       VMeta F{};
       if (pf != 0xffffffffu) {
-        F = meta_at(pf);
+        if constexpr (kMeta) F = meta_at(pf);
+        else F = FP[lv - 1];
         if (ROUTE && v.lvl_sliced[lv] >= 0 && F.data != nullptr) {
           gline = F.line0 + fastmod(h, F.L, F.magic);
         } else if (F.data == nullptr) {
