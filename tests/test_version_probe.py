@@ -455,3 +455,22 @@ def test_oracle_random_shapes_consistent():
     cand, lf2 = oracle.version_probe(nofilt, q, n, snapshot=1 << 51)
     assert np.array_equal(lf, lf2)
     assert np.all((mask & ~cand) == 0) and cand.any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [2, 3, 4, 5])
+def test_gpu_version_tiers_forced(mode):
+    """Every table tier on small and random versions (one file, three, up to a
+    few hundred, no level-0 files, empty levels): DLSM_VERSION_LDS=2..5 forces
+    the metadata + prefixes, metadata + sparse index, sparse index only and
+    nothing-in-LDS tiers (the variable is read once per process, so each tier
+    runs in a child process of its own, one after another)."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DLSM_VERSION_LDS=str(mode))
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "_version_tier_check.py")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.strip().splitlines()[-1] == "ok 5"
