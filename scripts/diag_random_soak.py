@@ -1,0 +1,87 @@
+"""Randomized soak of the version probe and the full probe against the oracle:
+the shapes of tests/test_version_probe.py::test_gpu_version_probe_random_shapes
+and tests/test_gpu_parity.py::test_full_probe_random_sets over many seeds
+(checker only: the oracle is test infrastructure).
+    python scripts/diag_random_soak.py [SEEDS]"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import torch  # noqa: E402
+
+import dlsm_amd  # noqa: E402
+import oracle  # noqa: E402
+from test_version_probe import random_version  # noqa: E402
+
+
+def version_case(ctx, seed):
+    rng = np.random.default_rng(10_000 + seed)
+    span = int(rng.integers(1_000, 5_000_000))
+    files = random_version(rng, int(rng.integers(0, 55)), span)
+    n = int(rng.integers(1, 300_000))
+    v_ = np.where(rng.random(n) < 0.5, rng.integers(0, span + 1, n),
+                  rng.integers(0, span + span // 5 + 2, n)).astype(np.uint64)
+    q = oracle.keys_from_values(v_)
+    snap = int(rng.integers(1, 1 << 52))
+    want, want_lf = oracle.version_probe(files, q, n, snapshot=snap)
+    v = ctx.version(files)
+    mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
+    lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
+    ctx.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
+    ctx.sync()
+    ok = np.array_equal(mask.cpu().numpy().view(np.uint64), want) and \
+        np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf)
+    v.close()
+    return ok, len(files)
+
+
+def probe_case(ctx, seed):
+    rng = np.random.default_rng(20_000 + seed)
+    F = int(rng.integers(1, 25))
+    key_len = int(rng.choice([16, 20, 24, 28, 33]))
+    equal = bool(rng.integers(0, 2))
+    n_eq = int(rng.integers(1, 300_000))
+    tabs = [rng.integers(0, 1 << 40, n_eq if equal else int(rng.integers(0, 300_000))).astype(np.uint64)
+            for _ in range(F)]
+    bpk = int(rng.integers(2, 21))
+    filters = [oracle.full_build(oracle.keys_from_values(t, key_len), t.size, stride=key_len,
+                                 bpk=bpk if equal else int(rng.integers(2, 21))) for t in tabs]
+    nq = int(rng.integers(1, 500_000))
+    pool = np.concatenate([t for t in tabs if t.size] + [np.zeros(1, np.uint64)])
+    vals = np.where(rng.random(nq) < 0.5, pool[rng.integers(0, pool.size, nq)],
+                    rng.integers(0, 1 << 40, nq).astype(np.uint64)).astype(np.uint64)
+    q = oracle.keys_from_values(vals, key_len)
+    want = oracle.full_probe(filters, q, nq, stride=key_len, nthreads=8)
+    fs = ctx.filterset(filters)
+    got = ctx.full_probe(fs, dlsm_amd.Keys(q, nq, key_len))
+    fs.close()
+    return np.array_equal(got, want), F
+
+
+def main():
+    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    ctx = dlsm_amd.Context(0)
+    bad = []
+    t0 = time.time()
+    for s in range(seeds):
+        ok, nf = version_case(ctx, s)
+        if not ok:
+            bad.append(("version", s, nf))
+        ok, F = probe_case(ctx, s)
+        if not ok:
+            bad.append(("probe", s, F))
+        if s % 10 == 9:
+            print(f"seed {s + 1}/{seeds}: {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
+    ctx.close()
+    print("soak:", seeds, "version cases,", seeds, "probe cases, mismatches:", bad, flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
