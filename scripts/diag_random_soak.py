@@ -1,7 +1,9 @@
-"""Randomized soak of the version probe and the full probe against the oracle:
-the shapes of tests/test_version_probe.py::test_gpu_version_probe_random_shapes
-and tests/test_gpu_parity.py::test_full_probe_random_sets over many seeds
-(checker only: the oracle is test infrastructure).
+"""Randomized soak of the version probe, the full probe and the full / legacy
+builds against the oracle: the shapes of
+tests/test_version_probe.py::test_gpu_version_probe_random_shapes and
+tests/test_gpu_parity.py::test_full_probe_random_sets over many seeds, and
+build batches of random table counts, sizes, duplicates, bits_per_key 1-24
+and key lengths (checker only: the oracle is test infrastructure).
     python scripts/diag_random_soak.py [SEEDS]"""
 import os
 import sys
@@ -64,6 +66,28 @@ def probe_case(ctx, seed):
     return np.array_equal(got, want), F
 
 
+def build_case(ctx, seed):
+    """A batch of 1-24 tables of 0-200 K keys (duplicates included), one
+    bits_per_key, one key length: full and legacy filters byte-equal."""
+    rng = np.random.default_rng(30_000 + seed)
+    T = int(rng.integers(1, 25))
+    key_len = int(rng.choice([16, 20, 24, 28, 33]))
+    bpk = int(rng.integers(1, 25))
+    tabs = []
+    for _ in range(T):
+        n = int(rng.integers(0, 200_000))
+        v = rng.integers(0, max(1, n // int(rng.integers(1, 4))) + 1, n).astype(np.uint64)  # some repeats
+        if rng.random() < 0.5:
+            v = np.sort(v)  # consecutive duplicates: AddKey's dedup
+        tabs.append(oracle.keys_from_values(v, key_len))
+    ns = [t.size // key_len for t in tabs]
+    got = ctx.full_build([dlsm_amd.Keys(t, n, key_len) for t, n in zip(tabs, ns)], bpk)
+    ok = all(g == oracle.full_build(t, n, stride=key_len, bpk=bpk) for g, t, n in zip(got, tabs, ns))
+    lg = ctx.legacy_build([dlsm_amd.Keys(t, n, key_len) for t, n in zip(tabs, ns)], bpk)
+    ok_l = all(g == oracle.legacy_build(t, n, stride=key_len, bpk=bpk) for g, t, n in zip(lg, tabs, ns))
+    return ok and ok_l, T
+
+
 def main():
     seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 100
     ctx = dlsm_amd.Context(0)
@@ -76,10 +100,14 @@ def main():
         ok, F = probe_case(ctx, s)
         if not ok:
             bad.append(("probe", s, F))
+        ok, T = build_case(ctx, s)
+        if not ok:
+            bad.append(("build", s, T))
         if s % 10 == 9:
             print(f"seed {s + 1}/{seeds}: {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
     ctx.close()
-    print("soak:", seeds, "version cases,", seeds, "probe cases, mismatches:", bad, flush=True)
+    print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy), mismatches:",
+          bad, flush=True)
     sys.exit(1 if bad else 0)
 
 
