@@ -88,6 +88,40 @@ def build_case(ctx, seed):
     return ok and ok_l, T
 
 
+def varlen_keys(rng, vals):
+    """Variable-length keys (0-40 bytes, a value's 8 bytes inside random
+    padding): data (16 zero bytes past the end) and offsets[n + 1]."""
+    n = vals.size
+    lens = rng.integers(0, 41, n)
+    parts = []
+    for v, l in zip(vals.tolist(), lens.tolist()):
+        b = int(v).to_bytes(8, "little") + bytes(rng.integers(0, 256, 32, dtype=np.uint8))
+        parts.append(b[:l])
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in parts])
+    data = np.frombuffer(b"".join(parts) + b"\0" * 16, dtype=np.uint8).copy()
+    return data, offs
+
+
+def varlen_case(ctx, seed):
+    """Variable-length keys: a build batch and a probe of its filters."""
+    rng = np.random.default_rng(40_000 + seed)
+    T = int(rng.integers(1, 10))
+    bpk = int(rng.integers(2, 21))
+    tabs = [varlen_keys(rng, rng.integers(0, 1 << 20, int(rng.integers(0, 60_000))).astype(np.uint64))
+            for _ in range(T)]
+    ns = [o.size - 1 for _, o in tabs]
+    got = ctx.full_build([dlsm_amd.Keys(d, n, 0, o) for (d, o), n in zip(tabs, ns)], bpk)
+    ok = all(g == oracle.full_build(d, n, offsets=o, bpk=bpk) for g, (d, o), n in zip(got, tabs, ns))
+    nq = int(rng.integers(1, 200_000))
+    qd, qo = varlen_keys(rng, rng.integers(0, 1 << 20, nq).astype(np.uint64))
+    want = oracle.full_probe(got, qd, nq, offsets=qo)
+    fs = ctx.filterset(got)
+    mask = ctx.full_probe(fs, dlsm_amd.Keys(qd, nq, 0, qo))
+    fs.close()
+    return ok and np.array_equal(mask, want), T
+
+
 def main():
     seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 100
     ctx = dlsm_amd.Context(0)
@@ -103,10 +137,14 @@ def main():
         ok, T = build_case(ctx, s)
         if not ok:
             bad.append(("build", s, T))
+        ok, T = varlen_case(ctx, s)
+        if not ok:
+            bad.append(("varlen", s, T))
         if s % 10 == 9:
             print(f"seed {s + 1}/{seeds}: {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
     ctx.close()
-    print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy), mismatches:",
+    print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy),", seeds,
+          "variable-length build + probe cases, mismatches:",
           bad, flush=True)
     sys.exit(1 if bad else 0)
 
