@@ -122,6 +122,31 @@ def varlen_case(ctx, seed):
     return ok and np.array_equal(mask, want), T
 
 
+def internal_case(ctx, seed):
+    """Internal keys (user key + 8-byte trailer, suffix_len 8): filters and
+    answers equal the user keys' (full_filter_block.cc hashes ExtractUserKey)."""
+    rng = np.random.default_rng(50_000 + seed)
+    T = int(rng.integers(1, 12))
+    ulen = int(rng.choice([16, 20, 24]))
+    bpk = int(rng.integers(2, 21))
+
+    def internal(u, n):
+        tr = rng.integers(0, 1 << 62, n).astype(np.uint64).view(np.uint8).reshape(n, 8)
+        return np.ascontiguousarray(np.concatenate([u.reshape(n, ulen), tr], axis=1).reshape(-1))
+
+    ns = [int(rng.integers(0, 150_000)) for _ in range(T)]
+    users = [oracle.keys_from_values(rng.integers(0, 1 << 30, n).astype(np.uint64), ulen) for n in ns]
+    got = ctx.full_build([dlsm_amd.Keys(internal(u, n), n, ulen + 8, suffix_len=8) for u, n in zip(users, ns)], bpk)
+    ok = all(g == oracle.full_build(u, n, stride=ulen, bpk=bpk) for g, u, n in zip(got, users, ns))
+    nq = int(rng.integers(1, 300_000))
+    qu = oracle.keys_from_values(rng.integers(0, 1 << 30, nq).astype(np.uint64), ulen)
+    want = oracle.full_probe(got, qu, nq, stride=ulen, nthreads=8)
+    fs = ctx.filterset(got)
+    mask = ctx.full_probe(fs, dlsm_amd.Keys(internal(qu, nq), nq, ulen + 8, suffix_len=8))
+    fs.close()
+    return ok and np.array_equal(mask, want), T
+
+
 def main():
     seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 100
     ctx = dlsm_amd.Context(0)
@@ -140,11 +165,14 @@ def main():
         ok, T = varlen_case(ctx, s)
         if not ok:
             bad.append(("varlen", s, T))
+        ok, T = internal_case(ctx, s)
+        if not ok:
+            bad.append(("internal", s, T))
         if s % 10 == 9:
             print(f"seed {s + 1}/{seeds}: {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
     ctx.close()
     print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy),", seeds,
-          "variable-length build + probe cases, mismatches:",
+          "variable-length and", seeds, "internal-key build + probe cases, mismatches:",
           bad, flush=True)
     sys.exit(1 if bad else 0)
 
