@@ -855,11 +855,18 @@ def e2e_hashed_rate(ctx, stream, tables, fs, qk, bpk, dev, ref, chunk_keys=12_50
     # hashed key's 4 B hash is written and read back by the DMA; against the
     # host's streaming read rate measured now, on the same cores
     host_bytes = 20 * K + 8 * hashed
+    # the cores' own share of those bytes: each hashed key's 20 B read and its
+    # 4 B hash written (the DMA engines read the rest); this is what the cores'
+    # read ceiling bounds
+    core_bytes = 24 * hashed
     host_read = host_read_rate(h_q)
     return {"mkeys_s": round(K / dt / 1e6, 1), "ms_per_step": round(dt * 1e3, 3),
             "host_bytes_per_step": host_bytes, "host_GBs": round(host_bytes / dt / 1e9, 2),
             "host_read_GBs_measured": host_read["GBs"], "host_read_method": host_read["method"],
             "frac_of_host_read": round(host_bytes / dt / 1e9 / host_read["GBs"], 4) if host_read["GBs"] else None,
+            "host_core_bytes_per_step": core_bytes, "host_core_GBs": round(core_bytes / dt / 1e9, 2),
+            "frac_of_host_read_cores": (round(core_bytes / dt / 1e9 / host_read["GBs"], 4)
+                                        if host_read["GBs"] else None),
             "ms_per_step_reps": [round(x * 1e3, 3) for x in times],
             "host_hashed_keys": hashed, "raw_keys": K - hashed,
             "host_hashed_tables": T - raw_t, "host_hashed_lookups": Q - raw_q,
