@@ -37,6 +37,7 @@ OPT_PATH, OPT_PROBE_ROUND_KEYS, OPT_BUILD_GROUPS = 0, 1, 2  # dlsm_ctx_set_optio
 OPT_PROBE_CHUNK_LG, OPT_PROBE_SLICE_LG, OPT_BUILD_EXACT, OPT_PROBE_ROUND_SERIAL = 3, 4, 5, 6
 OPT_FAULT_INJECT = 7  # test hook: builds / probes on the context return -value
 OPT_VERSION_SLICE_BYTES, OPT_VERSION_PASS_SLICES = 8, 9  # sliced version probe: level threshold, slices per pass
+OPT_PROBE_MULTI = 10  # multi-group filter sets: 1 one pass over every group (default), 0 a pass per group
 
 
 def lib():

@@ -87,8 +87,22 @@ uint32_t ceil_div_u32(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a 
 constexpr int kProbeBufs = 3;
 constexpr int kStageEvents = 4;
 
+// The scheduling options a pooled context starts with; a recycled context gets
+// them back (a thread may have changed them, e.g. a builder's BUILD_EXACT).
+// Kept inside the context itself: a detached thread that exits after main
+// returns still recycles its context safely (no static map to outlive).
+struct CtxOpts {
+  int path, build_groups;
+  uint64_t probe_round;
+  int probe_lgc, probe_lgr, build_exact;
+  bool probe_serial;
+  int probe_multi;
+};
+
 struct dlsm_ctx {
   int device = 0;
+  CtxOpts opts0{};          // creation options (pooled thread contexts)
+  bool opts0_set = false;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   hipStream_t aux = nullptr;              // helper stream of the pipelined passes
@@ -109,6 +123,7 @@ struct dlsm_ctx {
   int build_exact = 0;       // DLSM_OPT_BUILD_EXACT: 0 auto, 1 always count first, 2 never
   bool probe_serial = false;  // DLSM_OPT_PROBE_ROUND_SERIAL: rounds one after another on one stream
   int fault = 0;              // DLSM_OPT_FAULT_INJECT: > 0 -> builds / probes return -fault
+  int probe_multi = 1;        // DLSM_OPT_PROBE_MULTI: 1 one pass over a multi-group set, 0 a pass per group
   uint64_t vslice_bytes = 0;  // DLSM_OPT_VERSION_SLICE_BYTES (0: default)
   uint32_t vpass_slices = kVMaxSlices;  // DLSM_OPT_VERSION_PASS_SLICES
   std::atomic<uint64_t> fallbacks{0};  // dlsm_fallback_note: host re-runs of this context's failed calls
@@ -208,6 +223,15 @@ struct ProbeGroup {
   uint32_t slotmap = 0;         // packed images: member m answers in bit (slotmap >> 4m) & 7
 };
 
+// One image-width class of a one-pass multi-group probe: the global slices
+// [s0, s0 + S) of the groups with image width lgw, walked by one slice launch
+// of wgs workgroups (plan: S + 1 workgroup starts at d_mgplan + plan_off).
+struct MGClass {
+  int lgw = 0, K = 0;  // K: 6 when every group of the class has k = 6, else 0 (run time k)
+  uint32_t s0 = 0, S = 0;
+  uint32_t plan_off = 0, wgs = 0;
+};
+
 struct dlsm_filterset {
   int device = 0;
   int F = 0;
@@ -221,6 +245,14 @@ struct dlsm_filterset {
   // (a filter in the reference's log2_cache_line_size_ == 0 branch)
   std::vector<ProbeGroup> groups;
   uint64_t stacked_bytes = 0;
+  // One-pass probe (2..kMGMaxGroups groups, every group sliceable at 128 KiB
+  // slices): the groups in slice order (by image width), their slices
+  // numbered globally, and one slice launch per width class.
+  MGroupDev* d_mg = nullptr;
+  uint32_t* d_mgplan = nullptr;
+  int mg_n = 0;
+  uint32_t mg_slices = 0;
+  std::vector<MGClass> mg_classes;
 };
 
 namespace {
@@ -483,16 +515,6 @@ CtxPool& ctx_pool() {
   static CtxPool* p = new CtxPool();  // intentionally leaked (see above)
   return *p;
 }
-// The scheduling options a context starts with; a recycled context gets them
-// back (a thread may have changed them, e.g. a builder's BUILD_EXACT).
-struct CtxOpts {
-  int path, build_groups;
-  uint64_t probe_round;
-  int probe_lgc, probe_lgr, build_exact;
-  bool probe_serial;
-};
-std::mutex g_opts_m;
-std::map<const dlsm_ctx*, CtxOpts> g_opts;  // creation options of pooled contexts
 void ctx_pool_put(dlsm_ctx* c);
 struct ThreadCtx {
   dlsm_ctx* owned = nullptr;
@@ -536,12 +558,12 @@ int dlsm_thread_ctx(dlsm_ctx** out) {
     }
     if (!t.owned) {
       DLSM_CHECK(dlsm_ctx_create(dev, &t.owned));
-      const CtxOpts o{t.owned->path, t.owned->build_groups, t.owned->probe_round, t.owned->probe_lgc,
-                      t.owned->probe_lgr, t.owned->build_exact, t.owned->probe_serial};
+      t.owned->opts0 = CtxOpts{t.owned->path,      t.owned->build_groups, t.owned->probe_round,
+                               t.owned->probe_lgc, t.owned->probe_lgr,    t.owned->build_exact,
+                               t.owned->probe_serial, t.owned->probe_multi};
+      t.owned->opts0_set = true;
       std::lock_guard<std::mutex> lk(p.m);
       p.created++;
-      std::lock_guard<std::mutex> lo(g_opts_m);
-      g_opts[t.owned] = o;
     }
   }
   *out = t.owned;
@@ -614,6 +636,7 @@ int dlsm_ctx_create(int device, dlsm_ctx** out) {
   if (const char* v = getenv("DLSM_PROBE_CHUNK_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_CHUNK_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SLICE_LG")) dlsm_ctx_set_option(ctx, DLSM_OPT_PROBE_SLICE_LG, strtoull(v, nullptr, 10));
   if (const char* v = getenv("DLSM_PROBE_SERIAL")) ctx->probe_serial = atoi(v) != 0;
+  if (const char* v = getenv("DLSM_PROBE_MULTI")) ctx->probe_multi = atoi(v) != 0;
   *out = ctx;
   return DLSM_OK;
 }
@@ -692,19 +715,17 @@ void ctx_pool_put(dlsm_ctx* c) {
   c->fault = 0;
   c->vslice_bytes = 0;
   c->vpass_slices = kVMaxSlices;
-  {
-    std::lock_guard<std::mutex> lo(g_opts_m);
-    auto it = g_opts.find(c);
-    if (it != g_opts.end()) {
-      const CtxOpts& o = it->second;
-      c->path = o.path;
-      c->build_groups = o.build_groups;
-      c->probe_round = o.probe_round;
-      c->probe_lgc = o.probe_lgc;
-      c->probe_lgr = o.probe_lgr;
-      c->build_exact = o.build_exact;
-      c->probe_serial = o.probe_serial;
-    }
+  c->fallbacks.store(0, std::memory_order_relaxed);  // the next thread's count starts at zero
+  if (c->opts0_set) {
+    const CtxOpts& o = c->opts0;
+    c->path = o.path;
+    c->build_groups = o.build_groups;
+    c->probe_round = o.probe_round;
+    c->probe_lgc = o.probe_lgc;
+    c->probe_lgr = o.probe_lgr;
+    c->build_exact = o.build_exact;
+    c->probe_serial = o.probe_serial;
+    c->probe_multi = o.probe_multi;
   }
   CtxPool& p = ctx_pool();
   std::lock_guard<std::mutex> lk(p.m);
@@ -800,6 +821,10 @@ int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value) {
       if (value < 1 || value > kVMaxSlices) return DLSM_E_ARG;
       ctx->vpass_slices = static_cast<uint32_t>(value);
       return DLSM_OK;
+    case DLSM_OPT_PROBE_MULTI:
+      if (value > 1) return DLSM_E_ARG;
+      ctx->probe_multi = static_cast<int>(value);
+      return DLSM_OK;
     default:
       return DLSM_E_ARG;
   }
@@ -818,6 +843,7 @@ int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value) {
     case DLSM_OPT_FAULT_INJECT: *value = static_cast<uint64_t>(ctx->fault); return DLSM_OK;
     case DLSM_OPT_VERSION_SLICE_BYTES: *value = ctx->vslice_bytes; return DLSM_OK;
     case DLSM_OPT_VERSION_PASS_SLICES: *value = ctx->vpass_slices; return DLSM_OK;
+    case DLSM_OPT_PROBE_MULTI: *value = static_cast<uint64_t>(ctx->probe_multi); return DLSM_OK;
     default: return DLSM_E_ARG;
   }
 }
@@ -1528,6 +1554,110 @@ int dlsm_user_keys_gather_dev(dlsm_ctx* ctx, const dlsm_keyset* ikeys, const uin
 // ---------------------------------------------------------------------------
 // Full filter probe
 // ---------------------------------------------------------------------------
+}  // extern "C"
+namespace {
+uint32_t device_cus_of(int dev) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  return static_cast<uint32_t>(n);
+}
+
+// The one-pass layout of a multi-group set (bloom_internal.h, MGroupDev): the
+// groups ordered by image width (one slice launch per width), every group cut
+// into full 128 KiB slices (2^(11 - lgw) lines), the slices numbered globally.
+// Each width class gets a workgroup plan over the CUs: a slice's share of the
+// workgroups is its share of the class's entries -- every lookup has one entry
+// per group, so slice s of group j (nl_s of L_j lines) expects nl_s / L_j of
+// them (a 3-slice group's slices get ~10x the workgroups of a 30-slice
+// group's).  A set that does not fit (a group with more than 256 slices, more
+// than kMGMaxSlices in all) keeps the per-group passes.  `s` is synchronised by
+// the caller before the host tables go out of scope.
+hipError_t mg_layout(dlsm_filterset* fs, hipStream_t s) {
+  const int G = static_cast<int>(fs->groups.size());
+  std::vector<int> order(G);
+  for (int j = 0; j < G; j++) order[j] = j;
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int a, int b) { return fs->groups[a].lgw < fs->groups[b].lgw; });
+  std::vector<MGroupDev> md;
+  uint32_t sbase = 0;
+  for (int j : order) {
+    const ProbeGroup& g = fs->groups[j];
+    const uint32_t R = 1u << (11 - g.lgw);
+    const uint32_t S = ceil_div_u32(g.L, R);
+    if (S < 1 || S > static_cast<uint32_t>(kMaxSlices) || !g.stacked) return hipSuccess;
+    MGroupDev d{};
+    d.image = reinterpret_cast<const uint8_t*>(g.stacked);
+    d.L = g.L;
+    d.magic = g.magic;
+    d.R = R;
+    d.rmagic = fastmod_magic(R);
+    d.S = S;
+    d.sbase = sbase;
+    d.slotmap = g.slotmap;
+    d.k = g.k;
+    d.lgw = g.lgw;
+    d.mask_byte = g.mask_byte;
+    md.push_back(d);
+    sbase += S;
+  }
+  if (sbase > kMGMaxSlices) return hipSuccess;
+  const uint32_t budget = device_cus_of(fs->device);
+  std::vector<uint32_t> plan;
+  std::vector<MGClass> classes;
+  for (int j = 0; j < G;) {
+    MGClass cl;
+    cl.lgw = md[j].lgw;
+    cl.s0 = md[j].sbase;
+    cl.K = 6;
+    std::vector<double> w;  // expected entry share per slice
+    int q = j;
+    for (; q < G && md[q].lgw == cl.lgw; q++) {
+      if (md[q].k != 6) cl.K = 0;
+      for (uint32_t t = 0; t < md[q].S; t++) {
+        const uint32_t nl = std::min(md[q].R, md[q].L - t * md[q].R);
+        w.push_back(static_cast<double>(nl) / md[q].L);
+      }
+    }
+    cl.S = static_cast<uint32_t>(w.size());
+    double W = 0;
+    for (double x : w) W += x;
+    std::vector<uint32_t> parts(cl.S);
+    std::vector<std::pair<double, uint32_t>> rem;
+    uint32_t used = 0;
+    for (uint32_t t = 0; t < cl.S; t++) {
+      const double want = budget * w[t] / W;
+      parts[t] = std::max<uint32_t>(1u, static_cast<uint32_t>(want));
+      used += parts[t];
+      rem.push_back({want - parts[t], t});
+    }
+    std::sort(rem.begin(), rem.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+    for (size_t r = 0; r < rem.size() && used < budget; r++, used++) parts[rem[r].second]++;
+    cl.plan_off = static_cast<uint32_t>(plan.size());
+    uint32_t acc = 0;
+    for (uint32_t t = 0; t < cl.S; t++) {
+      plan.push_back(acc);
+      acc += parts[t];
+    }
+    plan.push_back(acc);
+    cl.wgs = acc;
+    classes.push_back(cl);
+    j = q;
+  }
+  hipError_t e = hipMalloc(reinterpret_cast<void**>(&fs->d_mg), sizeof(MGroupDev) * md.size());
+  if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&fs->d_mgplan), sizeof(uint32_t) * plan.size());
+  if (e == hipSuccess) e = hipMemcpy(fs->d_mg, md.data(), sizeof(MGroupDev) * md.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(fs->d_mgplan, plan.data(), sizeof(uint32_t) * plan.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return e;
+  (void)s;
+  fs->mg_n = G;
+  fs->mg_slices = sbase;
+  fs->mg_classes = classes;
+  return hipSuccess;
+}
+}  // namespace
+extern "C" {
+
 int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const uint64_t* lens,
                           int n_filters, int filters_are_device, dlsm_filterset** out) {
   if (!ctx || !out || !filters || !lens || n_filters < 1 || n_filters > 64) return DLSM_E_ARG;
@@ -1631,7 +1761,8 @@ int dlsm_filterset_create(dlsm_ctx* ctx, const uint8_t* const* filters, const ui
       fs->stacked_bytes += bytes;
     }
   }
-  if (e == hipSuccess) e = hipStreamSynchronize(s);  // `slots` is pageable host memory
+  if (e == hipSuccess && G >= 2 && G <= static_cast<size_t>(kMGMaxGroups)) e = mg_layout(fs, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);  // `slots` (and mg_layout's tables) are pageable host memory
   if (e != hipSuccess) {
     dlsm_filterset_destroy(fs);
     return from_hip(e);
@@ -1645,6 +1776,8 @@ int dlsm_filterset_destroy(dlsm_filterset* fs) {
   DeviceGuard g(fs->device);
   for (auto& grp : fs->groups)
     if (grp.stacked) (void)hipFree(grp.stacked);
+  if (fs->d_mg) (void)hipFree(fs->d_mg);
+  if (fs->d_mgplan) (void)hipFree(fs->d_mgplan);
   if (fs->d_slots) (void)hipFree(fs->d_slots);
   if (fs->d_filters) (void)hipFree(fs->d_filters);
   if (fs->blob) (void)hipFree(fs->blob);
@@ -1771,6 +1904,36 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
   return DLSM_OK;
 }
 
+// A multi-group set in ONE pass (dlsm_filterset::d_mg): one partition that
+// reads and hashes each lookup once and buckets it by every group's slice, one
+// slice launch per image-width class over all of the class's slices, one
+// unpermute that assembles every mask byte.  Per lookup: 20 B key in, G x
+// (4 B entry + 2 B position) out; G x 4 B in, G x 1 B out; G x 3 B in, the
+// mask bytes out -- against the per-group passes' hash pass plus G x
+// (4 B hash in + 6 B out, 5 B, 3 B + a mask read-modify-write).
+int probe_multi(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, int mode, uint8_t* mask_dev) {
+  hipStream_t s = ctx->stream;
+  const uint64_t n = kd.n;
+  const int G = fs->mg_n;
+  const int lgC = mg_chunk_lg(G);
+  const uint64_t C = 1ull << lgC;
+  const uint64_t nC = (n + C - 1) >> lgC;
+  const uint32_t region = mg_region(G, static_cast<uint32_t>(C), fs->mg_slices);
+  DLSM_CHECK(ctx->entries.ensure(nC * region));
+  DLSM_CHECK(ctx->smask.ensure(nC * region));
+  DLSM_CHECK(ctx->pos.ensure(nC * G * C));
+  DLSM_CHECK(ctx->tab.ensure(nC * (fs->mg_slices + 1)));
+  DLSM_TRY(launch_probe_mpartition(kd, fs->d_mg, G, fs->mg_slices, region, ctx->entries.p, ctx->pos.p,
+                                   ctx->tab.p, mode, s));
+  for (const MGClass& cl : fs->mg_classes)
+    DLSM_TRY(launch_probe_mslices(cl.lgw, cl.K, fs->d_mg, G, cl.s0, cl.S, fs->mg_slices, region,
+                                  static_cast<uint32_t>(nC), ctx->entries.p, ctx->tab.p, ctx->smask.p,
+                                  fs->d_mgplan + cl.plan_off, cl.wgs, s));
+  DLSM_TRY(launch_probe_munpermute(n, fs->d_mg, G, fs->mg_slices, region, ctx->pos.p, ctx->smask.p, mask_dev,
+                                   (fs->F + 7) / 8, s));
+  return DLSM_OK;
+}
+
 }  // namespace
 
 namespace {
@@ -1804,6 +1967,9 @@ int full_probe_dev_impl(dlsm_ctx* ctx, const dlsm_filterset* fs, const dlsm_keys
     DLSM_TRY(launch_probe_direct(fs->d_filters, fs->F, kd, mask_dev, mode, s));
     return DLSM_OK;
   }
+  if (fs->mg_n > 0 && ctx->probe_multi && fs->groups.size() > 1 &&
+      keys->n <= (0xffffffffull << mg_chunk_lg(fs->mg_n)))
+    return probe_multi(ctx, fs, kd, mode, mask_dev);
   if (fs->groups.size() > 1 || !all_sliceable) return probe_grouped(ctx, fs, kd, mode, mask_dev);
 
   // One group (the bench's set: <= 8 filters of one line count): the keys are
@@ -2177,6 +2343,12 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
   }
   const uint32_t n_bnd = static_cast<uint32_t>(bnd.size());
   std::vector<VIntervalDev> ivl(n_bnd + 1);
+  // FindFile's pick per level as a two-pointer sweep: right(j) = the first
+  // file r < count-1 whose largest has prefix index >= j (else count-1); the
+  // set of such r only shrinks as j grows, so right(j) never decreases and
+  // each level is walked once over all j (O(n_bnd + files), not O(n_bnd x
+  // files): a 60,000-file level took seconds per version before).
+  uint32_t rgt[kNumLevels] = {};
   for (uint32_t j = 0; j <= n_bnd; j++) {
     VIntervalDev& r = ivl[j];
     r.l0mask = 0;
@@ -2188,7 +2360,7 @@ int dlsm_version_create(dlsm_ctx* ctx, const dlsm_version_file* files, int n_fil
       if (!count[lv] || begin[lv] + count[lv] > 0xffffu) continue;  // (> 65,535 files: never read)
       // FindFile (version_set.cc:95-118): files [0, count-1) whose largest
       // sorts below the lookup come first; right starts at count-1
-      uint32_t right = 0;
+      uint32_t& right = rgt[lv];
       while (right < count[lv] - 1 && il[begin[lv] + right] < j) right++;
       if (is[begin[lv] + right] < j) r.pick[lv - 1] = static_cast<uint16_t>(begin[lv] + right);
     }

@@ -247,6 +247,48 @@ hipError_t launch_probe_slices(const uint64_t* stacked, uint32_t L, uint32_t mag
 hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const uint8_t* smask,
                                   uint8_t* mask, int lgC, hipStream_t s);
 
+// ---- one-pass probe of a multi-group filter set (round 6) -------------------
+// A Version's filters differ in line count (flush outputs, size-capped
+// compaction outputs, dedup-shifted L), so its filter set splits into groups
+// of one (L, k).  The one-pass probe hashes each lookup once in ONE partition
+// pass that buckets it by every group's slice: a chunk's region holds the
+// groups' bucket runs back to back (group j's buckets are the global slices
+// [sbase_j, sbase_j + S_j)), and one table row of S_tot + 1 u16 offsets per
+// chunk covers them all; the slice pass walks every group's slices (one launch
+// per image width class) and one unpermute ORs every group's answer byte into
+// the key's mask bytes.
+struct MGroupDev {
+  const uint8_t* image;  // stacked (lgw 3) or packed image, 64 * 2^lgw bytes per line
+  uint32_t L, magic;     // line count + fastmod magic
+  uint32_t R, rmagic;    // lines per slice (2^(11 - lgw): 128 KiB) + fastdivmod magic
+  uint32_t S, sbase;     // slices; the group's first global slice
+  uint32_t slotmap;      // packed images: member m answers in bit (slotmap >> 4m) & 7
+  int32_t k, lgw, mask_byte;
+};
+constexpr int kMGMaxGroups = 16;
+constexpr uint32_t kMGMaxSlices = 1024;
+// Keys per chunk of the one-pass partition: G * C answer entries per chunk
+// region (u16 offsets and positions), so larger sets take smaller chunks.
+constexpr int mg_chunk_lg(int G) { return G <= 8 ? 12 : 11; }
+// u32 entries (and answer bytes) per chunk region: every group's C entries
+// plus up to 3 pads per bucket, a multiple of 4 (16-byte units).
+constexpr uint32_t mg_region(int G, uint32_t C, uint32_t S_tot) {
+  return static_cast<uint32_t>(G) * C + 4u * S_tot;
+}
+hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t S_tot,
+                                   uint32_t region, uint32_t* entries, uint16_t* pos, uint16_t* tab, int mode,
+                                   hipStream_t s);
+// The slices [s0, s0 + S) of one image-width class (every group with image
+// width lgw; K: 6 when every such group has k = 6, else 0 = the group's k),
+// workgroups per slice from plan (S + 1 starts, wgs = plan[S]).
+hipError_t launch_probe_mslices(int lgw, int K, const MGroupDev* groups, int G, uint32_t s0, uint32_t S,
+                                uint32_t S_tot, uint32_t region, uint32_t n_chunks, const uint32_t* entries,
+                                const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
+                                hipStream_t s);
+hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t S_tot,
+                                   uint32_t region, const uint16_t* pos, const uint8_t* smask, uint8_t* mask,
+                                   int mask_bytes, hipStream_t s);
+
 hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
                                 uint64_t* slot_mask, uint32_t* level_file, hipStream_t s);
 // Route pass of the sliced version probe: launch_version_probe's outputs for

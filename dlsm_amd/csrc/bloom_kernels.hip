@@ -570,6 +570,8 @@ struct SegWalk {
   uint32_t excl, dv, T;
   uint64_t nz;        // non-empty segments of the current group
   uint32_t nrow;      // prefetched table row pair of group g + g_step (this lane's chunk), packed
+  uint32_t chunk_rt;  // CHUNK == 0: the chunk region stride in elements, known at run time only
+  __device__ __forceinline__ uint32_t stride() const { return CHUNK ? CHUNK : chunk_rt; }
 
   // The row pair (bucket start, bucket end) of this lane's chunk as one
   // packed u32, unpacked only in setup(): the load stays in flight until the
@@ -587,7 +589,7 @@ struct SegWalk {
     const uint32_t incl = wave_incl_scan_dpp(cnt);
     excl = incl - cnt;
     T = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    dv = lane * CHUNK + a0 - excl;
+    dv = lane * stride() + a0 - excl;
     nz = uniform64(__ballot(cnt != 0u));
     e0 = 0;
     if (cnt != 0u) {  // compact the non-empty segments' dv (ordered by lane = by excl)
@@ -651,7 +653,7 @@ struct SegWalk {
     return true;
   }
   __device__ __forceinline__ void fetch(const uint32_t (&idx)[U], uint32_t gset, E (&hv)[U]) const {
-    const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * CHUNK;
+    const E* gent = reinterpret_cast<const E*>(entries) + static_cast<uint64_t>(gset) * stride();
 #pragma unroll
     for (int u = 0; u < U; u++) {  // in-group for every lane: no select around the load
       if constexpr (NTL && sizeof(E) == 16) {
@@ -686,9 +688,11 @@ template <int U, uint32_t CHUNK, typename E = uint32_t, int DEPTH = 1, bool NTL 
           typename Pro = NoPrologue>
 __device__ __forceinline__ void walk_segments(const uint16_t* tb, uint32_t rowlen, const uint32_t* entries,
                                               uint32_t g_first, uint32_t g_step, uint32_t g_end, uint32_t gs,
-                                              uint32_t* scratch, Act act, Pro pro = Pro{}) {
+                                              uint32_t* scratch, Act act, Pro pro = Pro{},
+                                              uint32_t chunk_rt = 0) {
   static_assert(DEPTH == 1 || DEPTH == 2, "walk depth");
   SegWalk<U, CHUNK, E, NTL> w{tb, entries, rowlen, g_step, g_end, gs};
+  w.chunk_rt = chunk_rt;
   w.scr = (lds_u32*)scratch;  // generic -> LDS address space (addrspacecast)
   uint32_t row0 = 0;
   const bool any = w.begin(g_first, row0);
@@ -1334,6 +1338,16 @@ __global__ __launch_bounds__(NT, (NT <= 512 && H > 1) ? 4 : 1) void probe_partit
   }
 }
 
+// A 16-byte load through a global-address-space pointer: an image pointer read
+// from a descriptor in memory (the one-pass probe's MGroupDev) is generic, and
+// generic (flat) loads of the slice made the compiler bounce them through
+// scratch.
+typedef __attribute__((address_space(1))) const u32x4 g_u32x4;
+__device__ __forceinline__ uint4 ld_global16(const uint4* p) {
+  const u32x4 x = *(g_u32x4*)(reinterpret_cast<uintptr_t>(p));
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
 // One probe of a packed image (LGW < 3): the W-bit field of position p in
 // the line at LDS byte `base`, shifted down to bit 0 (higher bits are the
 // next fields: the caller masks after the AND of the k probes).
@@ -1363,11 +1377,18 @@ __device__ __forceinline__ uint32_t packed_answer(uint32_t acc, uint32_t slotmap
 // plan (nullptr: every slice has `parts` parts): S+1 workgroup starts, slice
 // s owning workgroups [plan[s], plan[s+1]) -- its parts, as many as its share
 // of the entries asks for (version_plan_kernel); workgroups past plan[S] exit.
-template <int LGR, int LGW, int K, int NT, int C, uint32_t CRE = probe_region(C)>
+// MG (one-pass multi-group probe): the launch covers global slices
+// [s0, s0 + S) of the groups mg[0, mg_n) (one image width LGW); each
+// workgroup's slice names its group, whose image, L, R, k and slotmap replace
+// the arguments; table rows hold `rowlen` offsets and chunk regions `cre_rt`
+// entries (both known at run time only).
+template <int LGR, int LGW, int K, int NT, int C, uint32_t CRE = probe_region(C), bool MG = false>
 __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     const uint8_t* __restrict__ stacked, uint32_t L, uint32_t Rs, uint32_t slotmap, int k, uint32_t S,
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
-    uint8_t* __restrict__ smask, int parts, const uint32_t* __restrict__ plan = nullptr) {
+    uint8_t* __restrict__ smask, int parts, const uint32_t* __restrict__ plan = nullptr,
+    const MGroupDev* __restrict__ mg = nullptr, int mg_n = 0, uint32_t s0 = 0, uint32_t rowlen = 0,
+    uint32_t cre_rt = 0) {
   // LDS holds up to R = 2^LGR lines; a slice is Rs <= R lines (Rs < R when the
   // slices are balanced so that S x parts fills the CUs exactly)
   constexpr uint32_t R = 1u << LGR;
@@ -1398,7 +1419,21 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     s = wi % S;
     p = wi / S;
   }
-  const uint32_t lo_line = s * Rs;
+  uint32_t lo_line = s * Rs;
+  if constexpr (MG) {
+    s += s0;  // global slice: the table column
+    int j = 0;
+    for (int q = 1; q < mg_n; q++)
+      if (mg[q].sbase <= s) j = q;  // groups in slice order
+    stacked = mg[j].image;
+    L = mg[j].L;
+    Rs = mg[j].R;
+    slotmap = mg[j].slotmap;
+    k = mg[j].k;
+    lo_line = (s - mg[j].sbase) * Rs;
+  } else {
+    rowlen = S + 1;
+  }
   const uint32_t nl = min(Rs, L - lo_line);
   // The slice into LDS: every 16-byte load in flight before the first LDS
   // store.  Loads AND stores are clamped (lanes past the slice rewrite its
@@ -1410,8 +1445,12 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint32_t nw = nl * (LB / 16);
   const uint32_t c_lo = static_cast<uint32_t>(static_cast<uint64_t>(p) * nC / parts);
   const uint32_t c_hi = static_cast<uint32_t>(static_cast<uint64_t>(p + 1) * nC / parts);
-  const uint16_t* tb = tab + s;  // chunk-major rows of S+1 u16
-  constexpr uint32_t CRU = CRE / 4;  // chunk region stride in 16-byte units
+  if constexpr (MG) {
+    if (c_lo >= c_hi) return;  // a plan sized for large batches: this part has no chunks (whole workgroup)
+  }
+  const uint16_t* tb = tab + s;  // chunk-major rows of `rowlen` u16
+  constexpr uint32_t CRU_C = MG ? 0u : CRE / 4;  // chunk region stride in 16-byte units (0: run time)
+  const uint32_t CRU = MG ? cre_rt / 4 : CRE / 4;
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
@@ -1479,27 +1518,28 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     auto slice_to_lds = [&] {
       uint4 t[V];
 #pragma unroll
-      for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
+      for (int v = 0; v < V; v++) t[v] = ld_global16(src + min(static_cast<uint32_t>(v * NT + tid), nw - 1u));
 #pragma unroll
       for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
       __syncthreads();
     };
-    walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
-        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
-        slice_to_lds);
+    walk_segments<U, CRU_C, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
+        tb, rowlen, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
+        slice_to_lds, CRU);
   } else {
     // packed images: the same load in front of the walk (as the walk's
     // prologue the compiler kept t[] in scratch for these shapes)
     {
       uint4 t[V];
 #pragma unroll
-      for (int v = 0; v < V; v++) t[v] = src[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)];
+      for (int v = 0; v < V; v++) t[v] = ld_global16(src + min(static_cast<uint32_t>(v * NT + tid), nw - 1u));
 #pragma unroll
       for (int v = 0; v < V; v++) dst[min(static_cast<uint32_t>(v * NT + tid), nw - 1u)] = t[v];
     }
     __syncthreads();
-    walk_segments<U, CRU, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
-        tb, S + 1, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set);
+    walk_segments<U, CRU_C, uint4, DLSM_PROBE_DEPTH, DLSM_PROBE_NTL != 0>(
+        tb, rowlen, entries, c_lo + wv * gs, NW * gs, c_hi, gs, walk_scr + wv * kWalkScratch, probe_set,
+        NoPrologue{}, CRU);
   }
 }
 
@@ -1571,6 +1611,176 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
       }
     } else {
       for (uint32_t i = i0; i < nk; i++) mask[first + i] = sm[pos[first + i]];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// One-pass probe of a multi-group filter set (round 6; bloom_internal.h,
+// MGroupDev).  Version::Get walks filters of many line counts
+// (db/version_set.cc:273-321): the set's groups each need their own bucketing,
+// but the keys are read and hashed ONCE here, and one slice pass and one
+// unpermute serve every group.
+// ---------------------------------------------------------------------------
+
+// Pass 1: one NT-thread workgroup per chunk of C keys.  The chunk is hashed
+// once into registers, then bucketed group by group (the group's LDS
+// histogram + ranks + block scan, as probe_partition_kernel does for one
+// group); group j's bucket runs go to [gbase_j, gbase_j + total_j) of the
+// chunk's region, so the region holds every group's runs back to back and one
+// table row of S_tot + 1 offsets (group j's slices at columns sbase_j..)
+// describes them all.  pos[(chunk * G + j) * C + i] = key i's entry position
+// in the region for group j.
+template <int MODE, int NT, int C>
+__global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const MGroupDev* __restrict__ groups,
+                                                              int G, uint32_t S_tot, uint32_t region,
+                                                              uint32_t* __restrict__ entries,
+                                                              uint16_t* __restrict__ pos,
+                                                              uint16_t* __restrict__ tab) {
+  constexpr int PER = C / NT;
+  constexpr uint32_t SR = C + 4u * kMaxSlices;  // one group's staged runs (C entries + pads)
+  constexpr int KB = mode_kb<MODE>();
+  using TL = K20Tile<NT, tile_kpt<KB>(), KB>;
+  constexpr int TV = TL::kVec > static_cast<int>(SR / 4) ? TL::kVec : static_cast<int>(SR / 4);
+  static_assert(PER % tile_kpt<KB>() == 0, "chunk shape");
+  __shared__ __attribute__((aligned(16))) uint4 tile[TV];  // key tiles, then a group's staged entries
+  __shared__ __attribute__((aligned(16))) uint16_t rk[C];   // rank in bucket, then region position
+  __shared__ uint8_t sb[C];                                 // slice inside the group (S_j <= 256)
+  __shared__ uint32_t hist[kMaxSlices + 1];
+  __shared__ uint8_t npad[kMaxSlices + 1];
+  __shared__ uint32_t wsum[NT / 64];
+  const int tid = threadIdx.x;
+  const uint32_t c = blockIdx.x;
+  const uint64_t first = static_cast<uint64_t>(c) * C;
+  const uint64_t left = kd.n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
+  uint32_t h[PER];
+  hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);
+  if constexpr (MODE == KM_HASH || MODE == KM_GENERIC) __syncthreads();  // (K20 / K28 end with one)
+  uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
+  uint16_t* trow = tab + static_cast<uint64_t>(c) * (S_tot + 1);
+  uint32_t* ereg = entries + static_cast<uint64_t>(c) * region;
+  uint32_t gbase = 0;
+  for (int j = 0; j < G; j++) {
+    // the group's constants (uniform: scalar loads)
+    const uint32_t L = groups[j].L, magic = groups[j].magic;
+    const uint32_t R = groups[j].R, rmagic = groups[j].rmagic;
+    const uint32_t S = groups[j].S, sbase = groups[j].sbase;
+    for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
+    __syncthreads();
+    uint32_t e[PER];
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + tid;
+      e[r] = 0;
+      if (i < nk) {
+        const uint32_t line = fastmod(h[r], L, magic);
+        uint32_t off;
+        const uint32_t sl = fastdivmod(line, R, rmagic, &off);
+        sb[i] = static_cast<uint8_t>(sl);
+        rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
+        e[r] = probe_entry(h[r], off);
+      }
+    }
+    __syncthreads();
+    for_buckets<NT>(S, [&](uint32_t b) {  // pad every bucket to whole 16-byte units
+      const uint32_t pad = (0u - hist[b]) & 3u;
+      npad[b] = static_cast<uint8_t>(pad);
+      hist[b] += pad;
+    });
+    __syncthreads();
+    const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
+    // group j's last offset is group j+1's first: only the last group writes it
+    for_buckets<NT>(j + 1 == G ? S + 1 : S, [&](uint32_t b) {
+      trow[sbase + b] = static_cast<uint16_t>(gbase + hist[b]);
+    });
+    for_buckets<NT>(S, [&](uint32_t b) {
+      const uint32_t end = hist[b + 1];
+      const uint32_t np = npad[b];
+      if (np > 0) stage[end - 1] = kProbePadEntry;
+      if (np > 1) stage[end - 2] = kProbePadEntry;
+      if (np > 2) stage[end - 3] = kProbePadEntry;
+    });
+#pragma unroll
+    for (int r = 0; r < PER; r++) {
+      const uint32_t i = r * NT + tid;
+      if (i < nk) {
+        const uint32_t p = hist[sb[i]] + rk[i];
+        stage[p] = e[r];
+        rk[i] = static_cast<uint16_t>(gbase + p);
+      }
+    }
+    __syncthreads();
+    store_chunk_u32<NT, true>(ereg + gbase, stage, total);
+    store_chunk_u16<NT, true>(pos + (static_cast<uint64_t>(c) * G + j) * C, rk, nk);
+    gbase += total;
+    __syncthreads();  // stage / rk / sb / hist reused by the next group
+  }
+}
+
+// Pass 3: one workgroup per chunk: the chunk's answer region (every group's
+// answer bytes, in bucket order) staged in LDS, then per key (8 per lane per
+// step) each group's answer byte gathered through its position and OR-ed into
+// the key's mask byte mask_byte_j (the slice pass already moved every member's
+// answer to its slot bit).  Every mask byte is written whole: no memset, no
+// read-modify-write.  MB: mask bytes per key (1 and 2 vectorized, 0 = any).
+template <int C, int MB>
+__global__ __launch_bounds__(kBlock) void probe_munpermute_kernel(uint64_t n, const MGroupDev* __restrict__ groups,
+                                                                  int G, uint32_t S_tot, uint32_t region,
+                                                                  const uint16_t* __restrict__ pos,
+                                                                  const uint8_t* __restrict__ smask,
+                                                                  uint8_t* __restrict__ mask, int mb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t msm[];
+  const int tid = threadIdx.x;
+  const uint32_t c = blockIdx.x;
+  const uint64_t first = static_cast<uint64_t>(c) * C;
+  const uint64_t left = n - first;
+  const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
+  const uint32_t used = min(region, static_cast<uint32_t>(G) * nk + 4u * S_tot);
+  const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(c) * region);
+  for (uint32_t v = tid; v < (used + 15u) / 16u; v += kBlock) reinterpret_cast<uint4*>(msm)[v] = s4[v];
+  __syncthreads();
+  const uint16_t* pc = pos + static_cast<uint64_t>(c) * G * C;
+  for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
+    if (i0 + 8u > nk) {  // the batch's ragged end: key by key
+      for (uint32_t i = i0; i < nk; i++) {
+        uint64_t a = 0;
+        for (int j = 0; j < G; j++)
+          a |= static_cast<uint64_t>(msm[pc[static_cast<uint64_t>(j) * C + i]]) << (8 * groups[j].mask_byte);
+        for (int b = 0; b < mb; b++) mask[(first + i) * static_cast<uint64_t>(mb) + b] = static_cast<uint8_t>(a >> (8 * b));
+      }
+      break;
+    }
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key i0 + q's mask bytes
+    for (int j = 0; j < G; j++) {
+      const uint32_t sh = 8u * static_cast<uint32_t>(groups[j].mask_byte);
+      const uint4 pv = load_pos8(pc + static_cast<uint64_t>(j) * C + i0);
+      const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        acc[2 * q] |= static_cast<uint64_t>(msm[pw[q] & 0xffffu]) << sh;
+        acc[2 * q + 1] |= static_cast<uint64_t>(msm[pw[q] >> 16]) << sh;
+      }
+    }
+    if constexpr (MB == 1) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        lo |= static_cast<uint32_t>(acc[q] & 0xffu) << (8 * q);
+        hi |= static_cast<uint32_t>(acc[q + 4] & 0xffu) << (8 * q);
+      }
+      *reinterpret_cast<uint2*>(mask + first + i0) = make_uint2(lo, hi);
+    } else if constexpr (MB == 2) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        w[q] = static_cast<uint32_t>(acc[2 * q] & 0xffffu) | (static_cast<uint32_t>(acc[2 * q + 1] & 0xffffu) << 16);
+      *reinterpret_cast<uint4*>(mask + 2 * (first + i0)) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; q++)
+        for (int b = 0; b < mb; b++)
+          mask[(first + i0 + q) * static_cast<uint64_t>(mb) + b] = static_cast<uint8_t>(acc[q] >> (8 * b));
     }
   }
 }
@@ -2795,6 +3005,25 @@ static uint32_t device_cus() {
   return c;
 }
 
+// Largest LDS allocation of one workgroup on device `dev` (cached per device
+// id like device_cus).
+static size_t device_lds_max(int dev) {
+  static std::atomic<uint32_t> lds[64] = {};
+  if (dev < 0 || dev >= 64) return 64u * 1024u;
+  uint32_t c = lds[dev].load(std::memory_order_relaxed);
+  if (!c) {
+    // the opt-in ceiling (what hipFuncAttributeMaxDynamicSharedMemorySize may
+    // raise a kernel to), else the default per-block one
+    int a = 0, b = 0;
+    if (hipDeviceGetAttribute(&a, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess) a = 0;
+    if (hipDeviceGetAttribute(&b, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess) b = 0;
+    const int n = std::max(std::max(a, b), 64 * 1024);
+    c = static_cast<uint32_t>(n);
+    lds[dev].store(c, std::memory_order_relaxed);
+  }
+  return c;
+}
+
 #ifndef DLSM_PROBE_P13_HALF
 #define DLSM_PROBE_P13_HALF 1
 #endif
@@ -3042,6 +3271,90 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
   return hipGetLastError();
 }
 
+// ---- one-pass multi-group probe launchers ----------------------------------
+hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t S_tot,
+                                   uint32_t region, uint32_t* entries, uint16_t* pos, uint16_t* tab, int mode,
+                                   hipStream_t s) {
+  if (keys.n == 0) return hipSuccess;
+  if (G < 1 || G > kMGMaxGroups || S_tot > kMGMaxSlices) return hipErrorInvalidValue;
+  const int lgC = mg_chunk_lg(G);
+  const uint64_t nC64 = (keys.n + (1ull << lgC) - 1) >> lgC;
+  if (nC64 > 0xffffffffull || mg_region(G, 1u << lgC, S_tot) > 65535u) return hipErrorInvalidValue;
+  const unsigned nC = static_cast<unsigned>(nC64);
+#define DLSM_MPART(MM, NT_, C_) \
+  probe_mpartition_kernel<MM, NT_, C_><<<nC, NT_, 0, s>>>(keys, groups, G, S_tot, region, entries, pos, tab)
+#define DLSM_MPART_C(NT_, C_)                          \
+  do {                                                 \
+    if (mode == KM_K20) DLSM_MPART(KM_K20, NT_, C_);   \
+    else if (mode == KM_K28) DLSM_MPART(KM_K28, NT_, C_); \
+    else if (mode == KM_HASH) DLSM_MPART(KM_HASH, NT_, C_); \
+    else DLSM_MPART(KM_GENERIC, NT_, C_);              \
+  } while (0)
+  if (lgC == 12) DLSM_MPART_C(512, 4096);
+  else DLSM_MPART_C(256, 2048);
+#undef DLSM_MPART_C
+#undef DLSM_MPART
+  return hipGetLastError();
+}
+
+template <int LGW, int K>
+static hipError_t probe_mslices_as(const MGroupDev* groups, int G, uint32_t s0, uint32_t S, uint32_t S_tot,
+                                   uint32_t region, uint32_t n_chunks, const uint32_t* entries,
+                                   const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
+                                   hipStream_t s) {
+  constexpr int NT = DLSM_PROBE_NT;
+  probe_slice_kernel<11 - LGW, LGW, K, NT, 0, 0u, true><<<wgs, NT, 0, s>>>(
+      nullptr, 0u, 0u, 0u, 0, S, n_chunks, entries, tab, smask, 1, plan, groups, G, s0, S_tot + 1, region);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe_mslices(int lgw, int K, const MGroupDev* groups, int G, uint32_t s0, uint32_t S,
+                                uint32_t S_tot, uint32_t region, uint32_t n_chunks, const uint32_t* entries,
+                                const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
+                                hipStream_t s) {
+  if (n_chunks == 0 || S == 0 || wgs == 0) return hipSuccess;
+  if (region % 4u != 0 || (K != 0 && K != 6)) return hipErrorInvalidValue;
+#define DLSM_MSL(LW)                                                                                              \
+  return K == 6 ? probe_mslices_as<LW, 6>(groups, G, s0, S, S_tot, region, n_chunks, entries, tab, smask, plan, \
+                                          wgs, s)                                                               \
+                : probe_mslices_as<LW, 0>(groups, G, s0, S, S_tot, region, n_chunks, entries, tab, smask, plan, \
+                                          wgs, s)
+  switch (lgw) {
+    case 0: DLSM_MSL(0);
+    case 1: DLSM_MSL(1);
+    case 2: DLSM_MSL(2);
+    case 3: DLSM_MSL(3);
+    default: return hipErrorInvalidValue;
+  }
+#undef DLSM_MSL
+}
+
+hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t S_tot,
+                                   uint32_t region, const uint16_t* pos, const uint8_t* smask, uint8_t* mask,
+                                   int mask_bytes, hipStream_t s) {
+  if (n_keys == 0) return hipSuccess;
+  if (mask_bytes < 1 || mask_bytes > 8) return hipErrorInvalidValue;
+  const int lgC = mg_chunk_lg(G);
+  const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(mask);
+  const int mbv = (mask_bytes == 1 && (a & 7u) == 0) ? 1 : (mask_bytes == 2 && (a & 15u) == 0) ? 2 : 0;
+  const size_t lds = (region + 15u) & ~15u;
+#define DLSM_MUNP(CC, MBV)                                                                                   \
+  probe_munpermute_kernel<CC, MBV><<<nC, kBlock, lds, s>>>(n_keys, groups, G, S_tot, region, pos, smask, mask, \
+                                                           mask_bytes)
+#define DLSM_MUNP_C(CC)               \
+  do {                                \
+    if (mbv == 1) DLSM_MUNP(CC, 1);   \
+    else if (mbv == 2) DLSM_MUNP(CC, 2); \
+    else DLSM_MUNP(CC, 0);            \
+  } while (0)
+  if (lgC == 12) DLSM_MUNP_C(4096);
+  else DLSM_MUNP_C(2048);
+#undef DLSM_MUNP_C
+#undef DLSM_MUNP
+  return hipGetLastError();
+}
+
 
 hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snapshot, uint64_t* slot_mask,
                                 uint32_t* level_file, uint32_t* hv, uint32_t* gl, hipStream_t s) {
@@ -3057,23 +3370,30 @@ hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snap
     const char* e = getenv("DLSM_VERSION_LDS");
     return e ? atoi(e) : 1;
   }();
+  // the LDS this device gives one workgroup (at most the kernel's 160 KiB)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const size_t lds_cap = std::min(kVLdsMax, device_lds_max(dev));
   int gt = lds_mode >= 2 ? std::min(lds_mode, 5) - 1 : 0;
-  while (gt < 4 && version_lds_bytes(v.n_bnd, nf, gt) > kVLdsMax) gt++;
+  while (gt < 4 && version_lds_bytes(v.n_bnd, nf, gt) > lds_cap) gt++;
   const size_t lds = version_lds_bytes(v.n_bnd, nf, gt);
   // a queued probe task names its file in 16 bits: larger versions take the
-  // lane-per-lookup kernel
-  if (lds_mode != 0 && lds <= kVLdsMax && nf <= 0xffffu) {
+  // lane-per-lookup kernel (as does a device whose LDS cannot hold even the
+  // wave queues)
+  if (lds_mode != 0 && lds <= lds_cap && nf <= 0xffffu && dev >= 0 && dev < 64) {
     // all files probed directly or through the queue share one probe count
     // in the common case (one bits_per_key): k = 6 unrolled
     const uint32_t g = static_cast<uint32_t>(std::min<uint64_t>((keys.n + kVRouteNT - 1) / kVRouteNT,
                                                                 static_cast<uint64_t>(device_cus())));
 #define DLSM_VLDS_GT(MM, RR, KK, GG)                                                                            \
   do {                                                                                                          \
-    static bool attr = false;                                                                                   \
-    if (!attr) {                                                                                                \
+    /* the dynamic-LDS ceiling, once per device (builder threads race here: */                                 \
+    /* the attribute call is idempotent, the flag word atomic) */                                               \
+    static std::atomic<uint64_t> attr{0};                                                                       \
+    if (!((attr.load(std::memory_order_acquire) >> dev) & 1u)) {                                                \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&version_lds_kernel<MM, RR, KK, GG>),             \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(kVLdsMax));       \
-      attr = true;                                                                                              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(lds_cap));        \
+      attr.fetch_or(uint64_t(1) << dev, std::memory_order_acq_rel);                                             \
     }                                                                                                           \
     version_lds_kernel<MM, RR, KK, GG><<<g, kVRouteNT, lds, s>>>(v, keys, snapshot, slot_mask, level_file, hv, gl, \
                                                                  nf);                                           \

@@ -198,6 +198,10 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *                             levels; UINT64_MAX: never)
  *   DLSM_OPT_VERSION_PASS_SLICES  128 KiB slices per partition pass of the sliced version
  *                             probe, 1..1024 (default 1024; larger levels take several)
+ *   DLSM_OPT_PROBE_MULTI      a filter set of several (L, k) groups (a Version's files of
+ *                             different sizes): 1 (default, or $DLSM_PROBE_MULTI) one
+ *                             partition + slice + unpermute pass over every group, 0 one
+ *                             such pass per group
  */
 #define DLSM_OPT_PATH 0
 #define DLSM_OPT_PROBE_ROUND_KEYS 1
@@ -209,6 +213,7 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
 #define DLSM_OPT_FAULT_INJECT 7
 #define DLSM_OPT_VERSION_SLICE_BYTES 8
 #define DLSM_OPT_VERSION_PASS_SLICES 9
+#define DLSM_OPT_PROBE_MULTI 10
 int dlsm_ctx_set_option(dlsm_ctx* ctx, int option, uint64_t value);
 /* The current value of an option (so a caller can restore it). */
 int dlsm_ctx_get_option(dlsm_ctx* ctx, int option, uint64_t* value);

@@ -67,8 +67,11 @@ def main():
         mask = torch.empty(Q * fs.mask_bytes, dtype=torch.uint8, device=dev)
         rec = {"shape": name, "filters": F, "keys_per_filter": sizes, "lookups": Q}
         ref_mask = None
-        for path, label in ((0, "auto"), (1, "direct")):
+        for path, label, multi in ((0, "auto", 1), (0, "per_group", 0), (1, "direct", 1)):
+            if label == "per_group" and len(set(sizes)) == 1:
+                continue
             ctx.set_path(path)
+            ctx.set_option(dlsm_amd.OPT_PROBE_MULTI, multi)
             ctx.full_probe_dev(fs, q, mask)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
@@ -83,6 +86,7 @@ def main():
                 ref_mask = m
             rec["paths_agree"] = bool(np.array_equal(ref_mask, m))
         ctx.set_path(0)
+        ctx.set_option(dlsm_amd.OPT_PROBE_MULTI, 1)
         if args.check:
             import oracle  # checker only
 

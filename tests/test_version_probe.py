@@ -339,13 +339,18 @@ def test_gpu_version_probe_many_files(gpu, l1_files):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nf", [5_000, 20_000, 70_000])
+@pytest.mark.parametrize("nf", [5_000, 20_000, 60_000, 70_000])
 def test_gpu_version_probe_more_files_than_task_bits(gpu, nf):
     """Versions past the LDS tables: 5,001 files keep only the sparse bound
     index in LDS (windows of 8 prefixes read from global memory), 20,001 keep
     nothing there, and more than 65,535 files -- a queued probe task names its
     file in 16 bits -- take the lane-per-lookup kernel; their answers equal
-    the oracle's like every other version's."""
+    the oracle's like every other version's.  Creating the version stays
+    linear in its files (the interval index's FindFile picks are a two-pointer
+    sweep per level: a 60,000-file level took seconds when every interval
+    re-walked the level)."""
+    import time
+
     import torch
 
     import dlsm_amd
@@ -358,11 +363,14 @@ def test_gpu_version_probe_more_files_than_task_bits(gpu, nf):
     q = oracle.keys_from_values(v_)
     snap = (1 << 56) - 1
     want, want_lf = oracle.version_probe(files, q, n, snapshot=snap)
+    t0 = time.perf_counter()
     v = gpu.version(files)
+    t_create = time.perf_counter() - t0
     mask = torch.zeros(n, dtype=torch.uint64, device="cuda")
     lf = torch.zeros((n, 5), dtype=torch.int32, device="cuda")
     gpu.version_probe_dev(v, dlsm_amd.Keys(torch.from_numpy(q).cuda(), n, 20), snap, mask, lf)
     gpu.sync()
+    assert t_create < 3.0, (nf, t_create)
     assert np.array_equal(mask.cpu().numpy().view(np.uint64), want), nf
     assert np.array_equal(lf.cpu().numpy().view(np.uint32), want_lf), nf
     v.close()
