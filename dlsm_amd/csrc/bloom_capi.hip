@@ -252,6 +252,9 @@ struct dlsm_filterset {
   uint32_t* d_mgplan = nullptr;
   int mg_n = 0;
   uint32_t mg_slices = 0;
+  uint32_t mg_region = 0;  // entries per chunk region (every group's sub-region)
+  uint32_t mg_abytes = 0;  // answer bytes per chunk
+  uint32_t mg_stage_bytes = 0;  // the partition's largest staging area (LDS)
   std::vector<MGClass> mg_classes;
 };
 
@@ -1601,6 +1604,26 @@ hipError_t mg_layout(dlsm_filterset* fs, hipStream_t s) {
     sbase += S;
   }
   if (sbase > kMGMaxSlices) return hipSuccess;
+  // every group's fixed sub-regions: entries, answers; its table columns
+  const uint32_t C = 1u << mg_chunk_lg(G);
+  uint32_t eoff = 0, aoff = 0;
+  for (int j = 0; j < G; j++) {
+    md[j].tcol = md[j].sbase + static_cast<uint32_t>(j);
+    md[j].eoff = eoff;
+    md[j].aoff = aoff;
+    eoff += mg_sub_entries(C, md[j].S);
+    aoff += mg_sub_abytes(C, md[j].S, md[j].lgw);
+  }
+  if (eoff > 65535u || aoff > 96u * 1024u) return hipSuccess;  // u16 table offsets / the unpermute's LDS
+  // the partition's staging LDS: the largest set of mg_set_size groups
+  const int P = mg_set_size(mg_chunk_lg(G));
+  uint32_t stage = 0;
+  for (int j0 = 0; j0 < G; j0 += P) {
+    uint32_t st = 0;
+    for (int j = j0; j < std::min(G, j0 + P); j++) st += mg_sub_entries(C, md[j].S) * 4u;
+    stage = std::max(stage, st);
+  }
+  if (stage > 64u * 1024u) return hipSuccess;
   const uint32_t budget = device_cus_of(fs->device);
   std::vector<uint32_t> plan;
   std::vector<MGClass> classes;
@@ -1652,6 +1675,9 @@ hipError_t mg_layout(dlsm_filterset* fs, hipStream_t s) {
   (void)s;
   fs->mg_n = G;
   fs->mg_slices = sbase;
+  fs->mg_region = eoff;
+  fs->mg_abytes = aoff;
+  fs->mg_stage_bytes = stage;
   fs->mg_classes = classes;
   return hipSuccess;
 }
@@ -1908,9 +1934,10 @@ int probe_grouped(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, in
 // reads and hashes each lookup once and buckets it by every group's slice, one
 // slice launch per image-width class over all of the class's slices, one
 // unpermute that assembles every mask byte.  Per lookup: 20 B key in, G x
-// (4 B entry + 2 B position) out; G x 4 B in, G x 1 B out; G x 3 B in, the
-// mask bytes out -- against the per-group passes' hash pass plus G x
-// (4 B hash in + 6 B out, 5 B, 3 B + a mask read-modify-write).
+// (4 B entry + 2 B position) out; G x 4 B in, G x W/8 B out (W: the group's
+// image field, 1..8 bits); G x (2 B + W/8 B) in, the mask bytes out --
+// against the per-group passes' hash pass plus G x (4 B hash in + 6 B out,
+// 5 B, 3 B + a mask read-modify-write).
 int probe_multi(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, int mode, uint8_t* mask_dev) {
   hipStream_t s = ctx->stream;
   const uint64_t n = kd.n;
@@ -1918,18 +1945,18 @@ int probe_multi(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, int 
   const int lgC = mg_chunk_lg(G);
   const uint64_t C = 1ull << lgC;
   const uint64_t nC = (n + C - 1) >> lgC;
-  const uint32_t region = mg_region(G, static_cast<uint32_t>(C), fs->mg_slices);
-  DLSM_CHECK(ctx->entries.ensure(nC * region));
-  DLSM_CHECK(ctx->smask.ensure(nC * region));
+  const uint32_t rowlen = fs->mg_slices + static_cast<uint32_t>(G);
+  DLSM_CHECK(ctx->entries.ensure(nC * fs->mg_region));
+  DLSM_CHECK(ctx->smask.ensure(nC * fs->mg_abytes));
   DLSM_CHECK(ctx->pos.ensure(nC * G * C));
-  DLSM_CHECK(ctx->tab.ensure(nC * (fs->mg_slices + 1)));
-  DLSM_TRY(launch_probe_mpartition(kd, fs->d_mg, G, fs->mg_slices, region, ctx->entries.p, ctx->pos.p,
-                                   ctx->tab.p, mode, s));
+  DLSM_CHECK(ctx->tab.ensure(nC * rowlen));
+  DLSM_TRY(launch_probe_mpartition(kd, fs->d_mg, G, rowlen, fs->mg_region, fs->mg_stage_bytes, ctx->entries.p,
+                                   ctx->pos.p, ctx->tab.p, mode, s));
   for (const MGClass& cl : fs->mg_classes)
-    DLSM_TRY(launch_probe_mslices(cl.lgw, cl.K, fs->d_mg, G, cl.s0, cl.S, fs->mg_slices, region,
+    DLSM_TRY(launch_probe_mslices(cl.lgw, cl.K, fs->d_mg, G, cl.s0, cl.S, rowlen, fs->mg_region, fs->mg_abytes,
                                   static_cast<uint32_t>(nC), ctx->entries.p, ctx->tab.p, ctx->smask.p,
                                   fs->d_mgplan + cl.plan_off, cl.wgs, s));
-  DLSM_TRY(launch_probe_munpermute(n, fs->d_mg, G, fs->mg_slices, region, ctx->pos.p, ctx->smask.p, mask_dev,
+  DLSM_TRY(launch_probe_munpermute(n, fs->d_mg, G, fs->mg_abytes, ctx->pos.p, ctx->smask.p, mask_dev,
                                    (fs->F + 7) / 8, s));
   return DLSM_OK;
 }

@@ -251,12 +251,20 @@ hipError_t launch_probe_unpermute(uint64_t n_keys, const uint16_t* pos, const ui
 // A Version's filters differ in line count (flush outputs, size-capped
 // compaction outputs, dedup-shifted L), so its filter set splits into groups
 // of one (L, k).  The one-pass probe hashes each lookup once in ONE partition
-// pass that buckets it by every group's slice: a chunk's region holds the
-// groups' bucket runs back to back (group j's buckets are the global slices
-// [sbase_j, sbase_j + S_j)), and one table row of S_tot + 1 u16 offsets per
-// chunk covers them all; the slice pass walks every group's slices (one launch
-// per image width class) and one unpermute ORs every group's answer byte into
-// the key's mask bytes.
+// pass that buckets it by every group's slice; the slice pass walks every
+// group's slices (one launch per image width class) and one unpermute ORs
+// every group's answer into the key's mask bytes.
+// Layout per chunk of C lookups:
+//  * entries: a region of `region` u32, group j's bucket runs in its own
+//    sub-region [eoff_j, eoff_j + C + 8 S_j) (every bucket padded to 8
+//    entries = two 16-byte units; the sub-region's tail is never written);
+//  * table: one row of S_tot + G u16 offsets (into the region), group j's
+//    S_j + 1 bucket starts at columns [tcol_j, tcol_j + S_j];
+//  * positions: pos[(chunk * G + j) * C + i] = key i's entry index inside
+//    group j's sub-region;
+//  * answers: W_j = 2^lgw_j bits per entry (the image's field: member m in
+//    bit m; a byte-wide stacked image's byte, slot-mapped already), group j's
+//    at byte aoff_j of the chunk's `abytes`-byte answer area.
 struct MGroupDev {
   const uint8_t* image;  // stacked (lgw 3) or packed image, 64 * 2^lgw bytes per line
   uint32_t L, magic;     // line count + fastmod magic
@@ -264,30 +272,44 @@ struct MGroupDev {
   uint32_t S, sbase;     // slices; the group's first global slice
   uint32_t slotmap;      // packed images: member m answers in bit (slotmap >> 4m) & 7
   int32_t k, lgw, mask_byte;
+  uint32_t tcol;         // first table column (sbase + the group's index)
+  uint32_t eoff;         // entry sub-region (u32 entries, a multiple of 8)
+  uint32_t aoff;         // answer sub-area (bytes, a multiple of 16)
+  uint32_t reserved;
 };
 constexpr int kMGMaxGroups = 16;
 constexpr uint32_t kMGMaxSlices = 1024;
-// Keys per chunk of the one-pass partition: G * C answer entries per chunk
-// region (u16 offsets and positions), so larger sets take smaller chunks.
-constexpr int mg_chunk_lg(int G) { return G <= 8 ? 12 : 11; }
-// u32 entries (and answer bytes) per chunk region: every group's C entries
-// plus up to 3 pads per bucket, a multiple of 4 (16-byte units).
-constexpr uint32_t mg_region(int G, uint32_t C, uint32_t S_tot) {
-  return static_cast<uint32_t>(G) * C + 4u * S_tot;
+constexpr uint32_t kMGPad = 8;  // entries per bucket padding unit (two 16-byte units: whole answer bytes at W = 1)
+// Keys per chunk of the one-pass partition (u16 table offsets into the chunk
+// region of G * C entries + padding), so larger sets take smaller chunks.
+#ifndef DLSM_MG_LG8
+#define DLSM_MG_LG8 11  // chunk lg for sets of <= 8 groups (A/B knob; 12: 4,096-key chunks)
+#endif
+constexpr int mg_chunk_lg(int G) { return G <= 8 ? DLSM_MG_LG8 : 11; }
+// Entries of group j's sub-region and bytes of its answer sub-area.
+constexpr uint32_t mg_sub_entries(uint32_t C, uint32_t S) { return C + kMGPad * S; }
+constexpr uint32_t mg_sub_abytes(uint32_t C, uint32_t S, int lgw) {
+  return (((mg_sub_entries(C, S) << lgw) / 8u) + 15u) & ~15u;
 }
-hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t S_tot,
-                                   uint32_t region, uint32_t* entries, uint16_t* pos, uint16_t* tab, int mode,
-                                   hipStream_t s);
+// stage_bytes: the largest staging area one set of the partition needs
+// (the sum of C + 8 S_j entries over the set's groups, x 4 bytes).
+hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t rowlen,
+                                   uint32_t region, uint32_t stage_bytes, uint32_t* entries, uint16_t* pos,
+                                   uint16_t* tab, int mode, hipStream_t s);
+#ifndef DLSM_MG_P
+#define DLSM_MG_P 2     // groups bucketed per phase of the partition (2,048-key chunks)
+#endif
+constexpr int mg_set_size(int lgC) { return lgC == 11 ? DLSM_MG_P : 2; }
 // The slices [s0, s0 + S) of one image-width class (every group with image
 // width lgw; K: 6 when every such group has k = 6, else 0 = the group's k),
 // workgroups per slice from plan (S + 1 starts, wgs = plan[S]).
 hipError_t launch_probe_mslices(int lgw, int K, const MGroupDev* groups, int G, uint32_t s0, uint32_t S,
-                                uint32_t S_tot, uint32_t region, uint32_t n_chunks, const uint32_t* entries,
-                                const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
-                                hipStream_t s);
-hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t S_tot,
-                                   uint32_t region, const uint16_t* pos, const uint8_t* smask, uint8_t* mask,
-                                   int mask_bytes, hipStream_t s);
+                                uint32_t rowlen, uint32_t region, uint32_t abytes, uint32_t n_chunks,
+                                const uint32_t* entries, const uint16_t* tab, uint8_t* answers,
+                                const uint32_t* plan, uint32_t wgs, hipStream_t s);
+hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t abytes,
+                                   const uint16_t* pos, const uint8_t* answers, uint8_t* mask, int mask_bytes,
+                                   hipStream_t s);
 
 hipError_t launch_version_probe(const VersionDev& v, KeyDesc keys, uint64_t snapshot,
                                 uint64_t* slot_mask, uint32_t* level_file, hipStream_t s);

@@ -1388,7 +1388,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     uint32_t nC, const uint32_t* __restrict__ entries, const uint16_t* __restrict__ tab,
     uint8_t* __restrict__ smask, int parts, const uint32_t* __restrict__ plan = nullptr,
     const MGroupDev* __restrict__ mg = nullptr, int mg_n = 0, uint32_t s0 = 0, uint32_t rowlen = 0,
-    uint32_t cre_rt = 0) {
+    uint32_t cre_rt = 0, uint32_t abytes = 0) {
   // LDS holds up to R = 2^LGR lines; a slice is Rs <= R lines (Rs < R when the
   // slices are balanced so that S x parts fills the CUs exactly)
   constexpr uint32_t R = 1u << LGR;
@@ -1420,8 +1420,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     p = wi / S;
   }
   uint32_t lo_line = s * Rs;
+  uint32_t eoffu = 0, aoff = 0;  // MG: the group's entry sub-region (units), answer sub-area (bytes)
   if constexpr (MG) {
-    s += s0;  // global slice: the table column
+    s += s0;  // global slice
     int j = 0;
     for (int q = 1; q < mg_n; q++)
       if (mg[q].sbase <= s) j = q;  // groups in slice order
@@ -1431,6 +1432,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
     slotmap = mg[j].slotmap;
     k = mg[j].k;
     lo_line = (s - mg[j].sbase) * Rs;
+    eoffu = mg[j].eoff / 4u;
+    aoff = mg[j].aoff;
+    s += static_cast<uint32_t>(j);  // the table column: every group has S_j + 1 columns
   } else {
     rowlen = S + 1;
   }
@@ -1451,6 +1455,7 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   const uint16_t* tb = tab + s;  // chunk-major rows of `rowlen` u16
   constexpr uint32_t CRU_C = MG ? 0u : CRE / 4;  // chunk region stride in 16-byte units (0: run time)
   const uint32_t CRU = MG ? cre_rt / 4 : CRE / 4;
+  const uint32_t cru_magic = MG ? fastmod_magic(CRU) : 0u;
   // Each lane takes one 16-byte unit (4 entries, bucket padding included) per
   // window, probes its 4 entries and writes their 4 answer bytes as one dword
   // (the answers mirror the entries' layout).
@@ -1458,6 +1463,84 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
   auto probe_set = [&](const uint4 (&hv)[U], const uint32_t (&idx)[U], const bool (&ok)[U], uint32_t g) {
         uint32_t* gmask = reinterpret_cast<uint32_t*>(smask) + static_cast<uint64_t>(g) * CRU;
         uint32_t ans[U];
+        if constexpr (MG) {
+          // One-pass probe: every unit's answers as W = 2^LGW bits per entry
+          // (the image's field; a stacked byte is slot-mapped already) at the
+          // group's answer sub-area: a 4W-bit value per unit, two units per
+          // byte at W = 1 (bucket runs are padded to pairs of units, so lanes
+          // 2m and 2m + 1 always hold the two units of one byte).
+          constexpr int NE = 4 * U;
+          constexpr uint32_t WM = LGW == 3 ? 0xffu : (1u << (1 << LGW)) - 1u;
+          uint32_t xs[NE], ds[NE], bs[NE], acc[NE];
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+              xs[4 * u + j] = e4[j];
+              ds[4 * u + j] = e4[j] >> 17;  // low 9 bits of rotr(h, 17)
+              bs[4 * u + j] = LGW == 3 ? (e4[j] & ((R - 1u) << 9)) : probe_entry_off(e4[j]) * LB;
+              acc[4 * u + j] = WM;
+            }
+          }
+          auto probe1 = [&](int n) -> uint32_t {
+            if constexpr (LGW == 3) return sl[bs[n] | (xs[n] & 511u)];
+            else return packed_probe<LGW>(sl, bs[n], xs[n]);
+          };
+          if constexpr (K > 0) {
+#pragma unroll
+            for (int q = 0; q < K; q++)
+#pragma unroll
+              for (int n = 0; n < NE; n++) {
+                acc[n] &= probe1(n);
+                xs[n] += ds[n];
+              }
+          } else {
+            for (int q = 0; q < k; q++)
+#pragma unroll
+              for (int n = 0; n < NE; n++) {
+                acc[n] &= probe1(n);
+                xs[n] += ds[n];
+              }
+          }
+          const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            uint32_t f = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) f |= (acc[4 * u + j] & WM) << (j << LGW);
+            uint32_t uo;
+            const uint32_t cq = fastdivmod(idx[u], CRU, cru_magic, &uo);
+            const uint32_t ul = uo - eoffu;  // the unit inside the group's sub-region
+            uint8_t* base = smask + static_cast<uint64_t>(g + cq) * abytes + aoff;
+            // Stores are unconditional (see below): a lane past the window's
+            // end holds a valid lane's unit and rewrites its answer.
+            if constexpr (LGW == 3) {
+              *reinterpret_cast<uint32_t*>(base + 4u * ul) = f;
+            } else if constexpr (LGW == 2) {
+              *reinterpret_cast<uint16_t*>(base + 2u * ul) = static_cast<uint16_t>(f);
+            } else if constexpr (LGW == 1) {
+              base[ul] = static_cast<uint8_t>(f);
+            } else {
+              // W = 1: the pair's byte from lanes 2m (low nibble) and 2m + 1; a
+              // lane past the window's end rewrites lanes 0 / 1's byte (its
+              // neighbour may hold another copy of lane 0's unit)
+              const uint32_t nb = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+                  0, static_cast<int>(f), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]: lane ^ 1
+              uint32_t pb = (lane & 1u) ? (nb | (f << 4)) : (f | (nb << 4));
+              uint64_t ad = reinterpret_cast<uint64_t>(base + (ul >> 1));
+              const uint32_t pb0 = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(pb), 0));
+              const uint32_t alo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ad), 0));
+              const uint32_t ahi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(ad >> 32), 0));
+              if (!ok[u]) {
+                pb = pb0;
+                ad = (static_cast<uint64_t>(ahi) << 32) | alo;
+              }
+              *reinterpret_cast<uint8_t*>(ad) = static_cast<uint8_t>(pb);
+            }
+          }
+          return;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
@@ -1623,130 +1706,246 @@ __global__ __launch_bounds__(kBlock) void probe_unpermute_kernel(uint64_t n,
 // unpermute serve every group.
 // ---------------------------------------------------------------------------
 
+// A full chunk's keys hashed into h[] (key r*NT+t -> thread t, h[r]) with
+// every load unconditional: tile rows past the tile are clamped to its last
+// 16 bytes (re-read, never stored), hashes come in as plain dwords.  Loads
+// under per-lane bounds checks made the compiler wait for each one right where
+// it was issued (a register copy merging the in-bounds and tail paths), one
+// HBM round trip per load.
+template <int MODE, int NT, int PER>
+__device__ __forceinline__ void hash_full_chunk(const KeyDesc& kd, uint64_t first, uint4* tile,
+                                                uint32_t (&h)[PER]) {
+  const int t = threadIdx.x;
+  if constexpr (MODE == KM_K20 || MODE == KM_K28) {
+    constexpr int KB = mode_kb<MODE>();
+    constexpr int KPT = tile_kpt<KB>();
+    using TL = K20Tile<NT, KPT, KB>;
+    constexpr int NTILES = PER / KPT;
+    const uint4* b4 = reinterpret_cast<const uint4*>(kd.bytes + first * KB);
+    uint4 all[NTILES][TL::kPer];
+#pragma unroll
+    for (int q = 0; q < NTILES; q++)
+#pragma unroll
+      for (int v = 0; v < TL::kPer; v++) {
+        const uint32_t u = min(static_cast<uint32_t>(v * NT + t), static_cast<uint32_t>(TL::kVec - 1));
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b4 + q * TL::kVec + u));
+        all[q][v] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+#pragma unroll
+    for (int q = 0; q < NTILES; q++) {
+#pragma unroll
+      for (int v = 0; v < TL::kPer; v++) {
+        const uint32_t u = v * NT + t;
+        if (TL::kVec % NT == 0 || u < static_cast<uint32_t>(TL::kVec)) tile[u] = all[q][v];
+      }
+      __syncthreads();
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(tile);
+#pragma unroll
+      for (int j = 0; j < KPT; j++) h[q * KPT + j] = hash_k20_lds(w + (KB / 4) * (j * NT + t));
+      __syncthreads();
+    }
+  } else if constexpr (MODE == KM_HASH) {
+    const uint32_t* hp = reinterpret_cast<const uint32_t*>(kd.bytes) + first;
+#pragma unroll
+    for (int r = 0; r < PER; r++) h[r] = __builtin_nontemporal_load(hp + r * NT + t);
+  } else {
+#pragma unroll
+    for (int r = 0; r < PER; r++) h[r] = key_hash<KM_GENERIC>(kd, first + r * NT + t);
+  }
+}
+
 // Pass 1: one NT-thread workgroup per chunk of C keys.  The chunk is hashed
-// once into registers, then bucketed group by group (the group's LDS
-// histogram + ranks + block scan, as probe_partition_kernel does for one
-// group); group j's bucket runs go to [gbase_j, gbase_j + total_j) of the
-// chunk's region, so the region holds every group's runs back to back and one
-// table row of S_tot + 1 offsets (group j's slices at columns sbase_j..)
-// describes them all.  pos[(chunk * G + j) * C + i] = key i's entry position
-// in the region for group j.
-template <int MODE, int NT, int C>
+// once into registers, then bucketed by every group (the group's LDS
+// histogram + ranks + scan, as probe_partition_kernel does for one group);
+// group j's bucket runs (each padded to kMGPad entries) go to its own
+// sub-region of the chunk's region, its S_j + 1 bucket starts to table
+// columns tcol_j.. of the chunk's row, and pos[(chunk * G + j) * C + i] =
+// key i's entry index inside the sub-region (bloom_internal.h, MGroupDev).
+// The groups are bucketed P at a time (the phases of a set run once: ranks,
+// scans, scatter, stores), every key's slice, rank and entry in registers (a
+// full chunk's rank atomics issue back to back, one LDS wait).  Three
+// barriers per set: after the ranks; after the scans -- wave p scans the
+// set's group p, writes its table row and padding and zeroes its histogram of
+// the next set (two sets of histograms alternate); after the scatter.  The
+// slices are 2^lgR lines (a power of two in the one-pass layout), so a line's
+// slice and offset are a shift and a mask.
+template <int MODE, int NT, int C, int P>
 __global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const MGroupDev* __restrict__ groups,
-                                                              int G, uint32_t S_tot, uint32_t region,
+                                                              int G, uint32_t rowlen, uint32_t region,
                                                               uint32_t* __restrict__ entries,
                                                               uint16_t* __restrict__ pos,
                                                               uint16_t* __restrict__ tab) {
   constexpr int PER = C / NT;
-  constexpr uint32_t SR = C + 4u * kMaxSlices;  // one group's staged runs (C entries + pads)
   constexpr int KB = mode_kb<MODE>();
-  using TL = K20Tile<NT, tile_kpt<KB>(), KB>;
-  constexpr int TV = TL::kVec > static_cast<int>(SR / 4) ? TL::kVec : static_cast<int>(SR / 4);
-  static_assert(PER % tile_kpt<KB>() == 0, "chunk shape");
-  __shared__ __attribute__((aligned(16))) uint4 tile[TV];  // key tiles, then a group's staged entries
-  __shared__ __attribute__((aligned(16))) uint16_t rk[C];   // rank in bucket, then region position
-  __shared__ uint8_t sb[C];                                 // slice inside the group (S_j <= 256)
-  __shared__ uint32_t hist[kMaxSlices + 1];
-  __shared__ uint8_t npad[kMaxSlices + 1];
-  __shared__ uint32_t wsum[NT / 64];
+  constexpr int QB = (kMaxSlices + 1 + 63) / 64;  // buckets per lane of a scanning wave
+  static_assert(PER % tile_kpt<KB>() == 0 && NT >= 64 * P, "chunk shape");
+  // key tiles, then the set's staged entries (group p of a set at the sum of
+  // the earlier groups' C + 8 S): dynamic LDS sized by the launcher for the
+  // filter set's largest set (mg_stage_bytes), so the occupancy follows the
+  // set's real padding, not the 256-slice worst case
+  extern __shared__ __attribute__((aligned(16))) uint4 tile[];
+  __shared__ __attribute__((aligned(16))) uint16_t rk[P][C];  // positions of the set's groups
+  __shared__ uint32_t hist[2 * P][kMaxSlices + 1];           // counts, then starts: P per set, 2 sets
   const int tid = threadIdx.x;
   const uint32_t c = blockIdx.x;
   const uint64_t first = static_cast<uint64_t>(c) * C;
   const uint64_t left = kd.n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
+  const bool full = nk == static_cast<uint32_t>(C);
+  for (uint32_t b = tid; b < P * (kMaxSlices + 1u); b += NT) (&hist[0][0])[b] = 0;  // (more than NT buckets)
   uint32_t h[PER];
-  hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);
-  if constexpr (MODE == KM_HASH || MODE == KM_GENERIC) __syncthreads();  // (K20 / K28 end with one)
+  if (full) hash_full_chunk<MODE, NT, PER>(kd, first, tile, h);
+  else hash_chunk<MODE, NT, PER>(kd, first, nk, tile, h);
+  __syncthreads();  // hist[0..P) zeroed (and, for hashes / generic keys, nothing else to wait for)
   uint32_t* stage = reinterpret_cast<uint32_t*>(tile);
-  uint16_t* trow = tab + static_cast<uint64_t>(c) * (S_tot + 1);
+  uint16_t* trow = tab + static_cast<uint64_t>(c) * rowlen;
   uint32_t* ereg = entries + static_cast<uint64_t>(c) * region;
-  uint32_t gbase = 0;
-  for (int j = 0; j < G; j++) {
-    // the group's constants (uniform: scalar loads)
-    const uint32_t L = groups[j].L, magic = groups[j].magic;
-    const uint32_t R = groups[j].R, rmagic = groups[j].rmagic;
-    const uint32_t S = groups[j].S, sbase = groups[j].sbase;
-    for_buckets<NT>(S + 1, [&](uint32_t b) { hist[b] = 0; });
-    __syncthreads();
-    uint32_t e[PER];
+  const uint32_t lane = tid & 63;
+  const int wv = wave_id();
+  for (int j0 = 0, q = 0; j0 < G; j0 += P, q ^= 1) {
+    const int np = min(P, G - j0);  // groups in this set (uniform)
+    uint32_t pk[P][PER], e[P][PER];   // (rank << 8) | slice; the entry
 #pragma unroll
-    for (int r = 0; r < PER; r++) {
-      const uint32_t i = r * NT + tid;
-      e[r] = 0;
-      if (i < nk) {
+    for (int pp = 0; pp < P; pp++) {
+      if (pp >= np) break;
+      const MGroupDev* gd = groups + j0 + pp;
+      const uint32_t L = gd->L, magic = gd->magic, R = gd->R;
+      const uint32_t lgR = static_cast<uint32_t>(__builtin_ctz(R));
+      uint32_t* hc = hist[P * q + pp];
+#pragma unroll
+      for (int r = 0; r < PER; r++) {
         const uint32_t line = fastmod(h[r], L, magic);
-        uint32_t off;
-        const uint32_t sl = fastdivmod(line, R, rmagic, &off);
-        sb[i] = static_cast<uint8_t>(sl);
-        rk[i] = static_cast<uint16_t>(atomicAdd(&hist[sl], 1u));
-        e[r] = probe_entry(h[r], off);
+        pk[pp][r] = line >> lgR;
+        e[pp][r] = probe_entry(h[r], line & (R - 1u));
       }
-    }
-    __syncthreads();
-    for_buckets<NT>(S, [&](uint32_t b) {  // pad every bucket to whole 16-byte units
-      const uint32_t pad = (0u - hist[b]) & 3u;
-      npad[b] = static_cast<uint8_t>(pad);
-      hist[b] += pad;
-    });
-    __syncthreads();
-    const uint32_t total = block_excl_scan_lds<NT>(hist, static_cast<int>(S + 1), wsum);
-    // group j's last offset is group j+1's first: only the last group writes it
-    for_buckets<NT>(j + 1 == G ? S + 1 : S, [&](uint32_t b) {
-      trow[sbase + b] = static_cast<uint16_t>(gbase + hist[b]);
-    });
-    for_buckets<NT>(S, [&](uint32_t b) {
-      const uint32_t end = hist[b + 1];
-      const uint32_t np = npad[b];
-      if (np > 0) stage[end - 1] = kProbePadEntry;
-      if (np > 1) stage[end - 2] = kProbePadEntry;
-      if (np > 2) stage[end - 3] = kProbePadEntry;
-    });
+      if (full) {
 #pragma unroll
-    for (int r = 0; r < PER; r++) {
-      const uint32_t i = r * NT + tid;
-      if (i < nk) {
-        const uint32_t p = hist[sb[i]] + rk[i];
-        stage[p] = e[r];
-        rk[i] = static_cast<uint16_t>(gbase + p);
+        for (int r = 0; r < PER; r++) pk[pp][r] |= atomicAdd(&hc[pk[pp][r]], 1u) << 8;
+      } else {
+#pragma unroll
+        for (int r = 0; r < PER; r++)
+          if (static_cast<uint32_t>(r * NT + tid) < nk) pk[pp][r] |= atomicAdd(&hc[pk[pp][r]], 1u) << 8;
       }
     }
     __syncthreads();
-    store_chunk_u32<NT, true>(ereg + gbase, stage, total);
-    store_chunk_u16<NT, true>(pos + (static_cast<uint64_t>(c) * G + j) * C, rk, nk);
-    gbase += total;
-    __syncthreads();  // stage / rk / sb / hist reused by the next group
+    if (wv < np) {
+      // wave p: exclusive scan of group j0+p's padded counts (QB buckets per
+      // lane), its table row and padding; its histogram of the next set zeroed
+      const int pp = wv;
+      const MGroupDev* gd = groups + j0 + pp;
+      const uint32_t S = gd->S, tcol = gd->tcol, eoff = gd->eoff;
+      uint32_t* hc = hist[P * q + pp];
+      uint32_t so = 0;  // the group's staging offset in the set
+      for (int o = 0; o < pp; o++) so += mg_sub_entries(C, groups[j0 + o].S);
+      uint32_t* st = stage + so;
+      uint32_t cnt[QB], pc[QB], loc = 0;
+#pragma unroll
+      for (int k = 0; k < QB; k++) {
+        const uint32_t b = QB * lane + k;
+        cnt[k] = b < S ? hc[b] : 0u;
+        pc[k] = (cnt[k] + (kMGPad - 1u)) & ~(kMGPad - 1u);
+        loc += pc[k];
+      }
+      const uint32_t incl = wave_incl_scan(loc);
+      uint32_t run = incl - loc;
+#pragma unroll
+      for (int k = 0; k < QB; k++) {
+        const uint32_t b = QB * lane + k;
+        if (b <= S) {
+          hc[b] = run;
+          trow[tcol + b] = static_cast<uint16_t>(eoff + run);
+        }
+        if (b < S)
+          for (uint32_t p = run + cnt[k]; p < run + pc[k]; p++) st[p] = kProbePadEntry;
+        run += pc[k];
+      }
+      if (j0 + P < G) {
+#pragma unroll
+        for (int k = 0; k < QB; k++)
+          if (QB * lane + k <= static_cast<uint32_t>(kMaxSlices)) hist[P * (q ^ 1) + pp][QB * lane + k] = 0u;
+      }
+    }
+    __syncthreads();
+    uint32_t so = 0;  // staging offset of the set's group pp
+#pragma unroll
+    for (int pp = 0; pp < P; pp++) {
+      if (pp >= np) break;
+      const uint32_t* hc = hist[P * q + pp];
+      uint32_t* st = stage + so;
+      so += mg_sub_entries(C, groups[j0 + pp].S);
+#pragma unroll
+      for (int r = 0; r < PER; r++) {
+        const uint32_t i = r * NT + tid;
+        if (full || i < nk) {
+          const uint32_t p = hc[pk[pp][r] & 0xffu] + (pk[pp][r] >> 8);
+          st[p] = e[pp][r];
+          rk[pp][i] = static_cast<uint16_t>(p);
+        }
+      }
+    }
+    __syncthreads();
+#ifndef DLSM_MG_ABL
+#define DLSM_MG_ABL 0  // ablation (timing only, wrong answers): 1 no entry stores, 2 no position stores
+#endif
+    so = 0;
+#pragma unroll
+    for (int pp = 0; pp < P; pp++) {
+      if (pp >= np) break;
+      const MGroupDev* gd = groups + j0 + pp;
+      if constexpr (!(DLSM_MG_ABL & 1)) store_chunk_u32<NT, true>(ereg + gd->eoff, stage + so, hist[P * q + pp][gd->S]);
+      if constexpr (!(DLSM_MG_ABL & 2)) store_chunk_u16<NT, true>(pos + (static_cast<uint64_t>(c) * G + j0 + pp) * C, rk[pp], nk);
+      so += mg_sub_entries(C, gd->S);
+    }
   }
 }
 
-// Pass 3: one workgroup per chunk: the chunk's answer region (every group's
-// answer bytes, in bucket order) staged in LDS, then per key (8 per lane per
-// step) each group's answer byte gathered through its position and OR-ed into
-// the key's mask byte mask_byte_j (the slice pass already moved every member's
-// answer to its slot bit).  Every mask byte is written whole: no memset, no
+// Pass 3: one workgroup per chunk: the chunk's answer area (every group's
+// W_j-bit answers) staged in LDS, then per key (8 per lane per step) each
+// group's answer field gathered through its position, mapped to its members'
+// slot bits (a 16-entry table per packed group; a byte-wide stacked image's
+// answer is the slot byte already) and OR-ed into the key's mask byte
+// mask_byte_j.  Every mask byte is written whole: no memset, no
 // read-modify-write.  MB: mask bytes per key (1 and 2 vectorized, 0 = any).
 template <int C, int MB>
 __global__ __launch_bounds__(kBlock) void probe_munpermute_kernel(uint64_t n, const MGroupDev* __restrict__ groups,
-                                                                  int G, uint32_t S_tot, uint32_t region,
+                                                                  int G, uint32_t abytes,
                                                                   const uint16_t* __restrict__ pos,
-                                                                  const uint8_t* __restrict__ smask,
+                                                                  const uint8_t* __restrict__ answers,
                                                                   uint8_t* __restrict__ mask, int mb) {
   extern __shared__ __attribute__((aligned(16))) uint8_t msm[];
+  __shared__ uint8_t lut[kMGMaxGroups][16];  // packed group j: W-bit field -> slot bits
   const int tid = threadIdx.x;
   const uint32_t c = blockIdx.x;
   const uint64_t first = static_cast<uint64_t>(c) * C;
   const uint64_t left = n - first;
   const uint32_t nk = left < static_cast<uint64_t>(C) ? static_cast<uint32_t>(left) : static_cast<uint32_t>(C);
-  const uint32_t used = min(region, static_cast<uint32_t>(G) * nk + 4u * S_tot);
-  const uint4* s4 = reinterpret_cast<const uint4*>(smask + static_cast<uint64_t>(c) * region);
-  for (uint32_t v = tid; v < (used + 15u) / 16u; v += kBlock) reinterpret_cast<uint4*>(msm)[v] = s4[v];
+  const uint4* s4 = reinterpret_cast<const uint4*>(answers + static_cast<uint64_t>(c) * abytes);
+  for (uint32_t v = tid; v < abytes / 16u; v += kBlock) reinterpret_cast<uint4*>(msm)[v] = s4[v];
+  if (tid < kMGMaxGroups * 16) {
+    const int j = tid >> 4;
+    const uint32_t f = tid & 15u;
+    uint32_t a = 0;
+    if (j < G && groups[j].lgw < 3) {
+      const uint32_t sm = groups[j].slotmap;
+      for (int m = 0; m < (1 << groups[j].lgw); m++) a |= ((f >> m) & 1u) << ((sm >> (4 * m)) & 7u);
+    }
+    lut[j][f] = static_cast<uint8_t>(a);
+  }
   __syncthreads();
   const uint16_t* pc = pos + static_cast<uint64_t>(c) * G * C;
+  // the answer field of group j's entry pl, mapped to slot bits
+  auto field = [&](int j, uint32_t lgw, uint32_t aoff, uint32_t pl) -> uint32_t {
+    if (lgw == 3) return msm[aoff + pl];
+    const uint32_t bit = pl << lgw;
+    return lut[j][(msm[aoff + (bit >> 3)] >> (bit & 7u)) & ((1u << (1u << lgw)) - 1u)];
+  };
   for (uint32_t i0 = 8u * tid; i0 < nk; i0 += 8u * kBlock) {
     if (i0 + 8u > nk) {  // the batch's ragged end: key by key
       for (uint32_t i = i0; i < nk; i++) {
         uint64_t a = 0;
         for (int j = 0; j < G; j++)
-          a |= static_cast<uint64_t>(msm[pc[static_cast<uint64_t>(j) * C + i]]) << (8 * groups[j].mask_byte);
+          a |= static_cast<uint64_t>(field(j, groups[j].lgw, groups[j].aoff, pc[static_cast<uint64_t>(j) * C + i]))
+               << (8 * groups[j].mask_byte);
         for (int b = 0; b < mb; b++) mask[(first + i) * static_cast<uint64_t>(mb) + b] = static_cast<uint8_t>(a >> (8 * b));
       }
       break;
@@ -1754,12 +1953,13 @@ __global__ __launch_bounds__(kBlock) void probe_munpermute_kernel(uint64_t n, co
     uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key i0 + q's mask bytes
     for (int j = 0; j < G; j++) {
       const uint32_t sh = 8u * static_cast<uint32_t>(groups[j].mask_byte);
+      const uint32_t lgw = static_cast<uint32_t>(groups[j].lgw), aoff = groups[j].aoff;
       const uint4 pv = load_pos8(pc + static_cast<uint64_t>(j) * C + i0);
       const uint32_t pw[4] = {pv.x, pv.y, pv.z, pv.w};
 #pragma unroll
       for (int q = 0; q < 4; q++) {
-        acc[2 * q] |= static_cast<uint64_t>(msm[pw[q] & 0xffffu]) << sh;
-        acc[2 * q + 1] |= static_cast<uint64_t>(msm[pw[q] >> 16]) << sh;
+        acc[2 * q] |= static_cast<uint64_t>(field(j, lgw, aoff, pw[q] & 0xffffu)) << sh;
+        acc[2 * q + 1] |= static_cast<uint64_t>(field(j, lgw, aoff, pw[q] >> 16)) << sh;
       }
     }
     if constexpr (MB == 1) {
@@ -3272,53 +3472,72 @@ hipError_t launch_probe_unpermute_group(uint64_t n_keys, const uint16_t* pos, co
 }
 
 // ---- one-pass multi-group probe launchers ----------------------------------
-hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t S_tot,
-                                   uint32_t region, uint32_t* entries, uint16_t* pos, uint16_t* tab, int mode,
-                                   hipStream_t s) {
+#ifndef DLSM_MG_NT
+#define DLSM_MG_NT 256  // partition threads per 2,048-key chunk
+#endif
+
+// Dynamic LDS of the one-pass partition: the key tiles or the largest set's
+// staged runs (stage_bytes, mg_layout), whichever is larger.
+template <int MODE, int NT, int C>
+static size_t mg_part_lds(uint32_t stage_bytes) {
+  constexpr int KB = MODE == KM_K28 ? 28 : 20;
+  using TL = K20Tile<NT, KB == 20 ? kTileKPT : 1, KB>;
+  return std::max<size_t>(static_cast<size_t>(TL::kVec) * 16u, stage_bytes);
+}
+
+hipError_t launch_probe_mpartition(KeyDesc keys, const MGroupDev* groups, int G, uint32_t rowlen,
+                                   uint32_t region, uint32_t stage_bytes, uint32_t* entries, uint16_t* pos,
+                                   uint16_t* tab, int mode, hipStream_t s) {
   if (keys.n == 0) return hipSuccess;
-  if (G < 1 || G > kMGMaxGroups || S_tot > kMGMaxSlices) return hipErrorInvalidValue;
+  if (stage_bytes > 64u * 1024u) return hipErrorInvalidValue;
+  if (G < 1 || G > kMGMaxGroups || rowlen > kMGMaxSlices + kMGMaxGroups || region > 65535u ||
+      region % kMGPad != 0)
+    return hipErrorInvalidValue;
   const int lgC = mg_chunk_lg(G);
   const uint64_t nC64 = (keys.n + (1ull << lgC) - 1) >> lgC;
-  if (nC64 > 0xffffffffull || mg_region(G, 1u << lgC, S_tot) > 65535u) return hipErrorInvalidValue;
+  if (nC64 > 0xffffffffull) return hipErrorInvalidValue;
   const unsigned nC = static_cast<unsigned>(nC64);
-#define DLSM_MPART(MM, NT_, C_) \
-  probe_mpartition_kernel<MM, NT_, C_><<<nC, NT_, 0, s>>>(keys, groups, G, S_tot, region, entries, pos, tab)
-#define DLSM_MPART_C(NT_, C_)                          \
-  do {                                                 \
-    if (mode == KM_K20) DLSM_MPART(KM_K20, NT_, C_);   \
-    else if (mode == KM_K28) DLSM_MPART(KM_K28, NT_, C_); \
-    else if (mode == KM_HASH) DLSM_MPART(KM_HASH, NT_, C_); \
-    else DLSM_MPART(KM_GENERIC, NT_, C_);              \
+#define DLSM_MPART(MM, NT_, C_, P_)                                                                            \
+  probe_mpartition_kernel<MM, NT_, C_, P_><<<nC, NT_, mg_part_lds<MM, NT_, C_>(stage_bytes), s>>>(               \
+      keys, groups, G, rowlen, region, entries, pos, tab)
+#define DLSM_MPART_C(NT_, C_, P_)                               \
+  do {                                                          \
+    if (mode == KM_K20) DLSM_MPART(KM_K20, NT_, C_, P_);        \
+    else if (mode == KM_K28) DLSM_MPART(KM_K28, NT_, C_, P_);   \
+    else if (mode == KM_HASH) DLSM_MPART(KM_HASH, NT_, C_, P_); \
+    else DLSM_MPART(KM_GENERIC, NT_, C_, P_);                   \
   } while (0)
-  if (lgC == 12) DLSM_MPART_C(512, 4096);
-  else DLSM_MPART_C(256, 2048);
+  // (shapes: bloom_internal.h mg_chunk_lg; A/B knobs DLSM_MG_NT / DLSM_MG_P)
+  if (lgC == 12) DLSM_MPART_C(512, 4096, 2);
+  else if (lgC == 11) DLSM_MPART_C(DLSM_MG_NT, 2048, mg_set_size(11));
+  else return hipErrorInvalidValue;
 #undef DLSM_MPART_C
 #undef DLSM_MPART
   return hipGetLastError();
 }
 
 template <int LGW, int K>
-static hipError_t probe_mslices_as(const MGroupDev* groups, int G, uint32_t s0, uint32_t S, uint32_t S_tot,
-                                   uint32_t region, uint32_t n_chunks, const uint32_t* entries,
-                                   const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
+static hipError_t probe_mslices_as(const MGroupDev* groups, int G, uint32_t s0, uint32_t S, uint32_t rowlen,
+                                   uint32_t region, uint32_t abytes, uint32_t n_chunks, const uint32_t* entries,
+                                   const uint16_t* tab, uint8_t* answers, const uint32_t* plan, uint32_t wgs,
                                    hipStream_t s) {
   constexpr int NT = DLSM_PROBE_NT;
   probe_slice_kernel<11 - LGW, LGW, K, NT, 0, 0u, true><<<wgs, NT, 0, s>>>(
-      nullptr, 0u, 0u, 0u, 0, S, n_chunks, entries, tab, smask, 1, plan, groups, G, s0, S_tot + 1, region);
+      nullptr, 0u, 0u, 0u, 0, S, n_chunks, entries, tab, answers, 1, plan, groups, G, s0, rowlen, region, abytes);
   return hipGetLastError();
 }
 
 hipError_t launch_probe_mslices(int lgw, int K, const MGroupDev* groups, int G, uint32_t s0, uint32_t S,
-                                uint32_t S_tot, uint32_t region, uint32_t n_chunks, const uint32_t* entries,
-                                const uint16_t* tab, uint8_t* smask, const uint32_t* plan, uint32_t wgs,
-                                hipStream_t s) {
+                                uint32_t rowlen, uint32_t region, uint32_t abytes, uint32_t n_chunks,
+                                const uint32_t* entries, const uint16_t* tab, uint8_t* answers,
+                                const uint32_t* plan, uint32_t wgs, hipStream_t s) {
   if (n_chunks == 0 || S == 0 || wgs == 0) return hipSuccess;
-  if (region % 4u != 0 || (K != 0 && K != 6)) return hipErrorInvalidValue;
-#define DLSM_MSL(LW)                                                                                              \
-  return K == 6 ? probe_mslices_as<LW, 6>(groups, G, s0, S, S_tot, region, n_chunks, entries, tab, smask, plan, \
-                                          wgs, s)                                                               \
-                : probe_mslices_as<LW, 0>(groups, G, s0, S, S_tot, region, n_chunks, entries, tab, smask, plan, \
-                                          wgs, s)
+  if (region % kMGPad != 0 || abytes % 16u != 0 || (K != 0 && K != 6)) return hipErrorInvalidValue;
+#define DLSM_MSL(LW)                                                                                          \
+  return K == 6 ? probe_mslices_as<LW, 6>(groups, G, s0, S, rowlen, region, abytes, n_chunks, entries, tab, \
+                                          answers, plan, wgs, s)                                            \
+                : probe_mslices_as<LW, 0>(groups, G, s0, S, rowlen, region, abytes, n_chunks, entries, tab, \
+                                          answers, plan, wgs, s)
   switch (lgw) {
     case 0: DLSM_MSL(0);
     case 1: DLSM_MSL(1);
@@ -3329,32 +3548,46 @@ hipError_t launch_probe_mslices(int lgw, int K, const MGroupDev* groups, int G, 
 #undef DLSM_MSL
 }
 
-hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t S_tot,
-                                   uint32_t region, const uint16_t* pos, const uint8_t* smask, uint8_t* mask,
-                                   int mask_bytes, hipStream_t s) {
+hipError_t launch_probe_munpermute(uint64_t n_keys, const MGroupDev* groups, int G, uint32_t abytes,
+                                   const uint16_t* pos, const uint8_t* answers, uint8_t* mask, int mask_bytes,
+                                   hipStream_t s) {
   if (n_keys == 0) return hipSuccess;
-  if (mask_bytes < 1 || mask_bytes > 8) return hipErrorInvalidValue;
+  if (mask_bytes < 1 || mask_bytes > 8 || abytes % 16u != 0 || abytes > 96u * 1024u) return hipErrorInvalidValue;
   const int lgC = mg_chunk_lg(G);
   const unsigned nC = static_cast<unsigned>((n_keys + (1ull << lgC) - 1) >> lgC);
   const uintptr_t a = reinterpret_cast<uintptr_t>(mask);
   const int mbv = (mask_bytes == 1 && (a & 7u) == 0) ? 1 : (mask_bytes == 2 && (a & 15u) == 0) ? 2 : 0;
-  const size_t lds = (region + 15u) & ~15u;
+  static std::atomic<uint64_t> attr{0};  // dynamic LDS past 64 KiB: once per device (idempotent)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (abytes > 64u * 1024u && dev >= 0 && dev < 64 && !((attr.load() >> dev) & 1u)) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&probe_munpermute_kernel<2048, 0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&probe_munpermute_kernel<2048, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&probe_munpermute_kernel<2048, 2>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    attr.fetch_or(uint64_t(1) << dev);
+  }
 #define DLSM_MUNP(CC, MBV)                                                                                   \
-  probe_munpermute_kernel<CC, MBV><<<nC, kBlock, lds, s>>>(n_keys, groups, G, S_tot, region, pos, smask, mask, \
-                                                           mask_bytes)
-#define DLSM_MUNP_C(CC)               \
-  do {                                \
-    if (mbv == 1) DLSM_MUNP(CC, 1);   \
+  probe_munpermute_kernel<CC, MBV><<<nC, kBlock, abytes, s>>>(n_keys, groups, G, abytes, pos, answers, mask, \
+                                                              mask_bytes)
+#define DLSM_MUNP_C(CC)                  \
+  do {                                   \
+    if (mbv == 1) DLSM_MUNP(CC, 1);      \
     else if (mbv == 2) DLSM_MUNP(CC, 2); \
-    else DLSM_MUNP(CC, 0);            \
+    else DLSM_MUNP(CC, 0);               \
   } while (0)
-  if (lgC == 12) DLSM_MUNP_C(4096);
-  else DLSM_MUNP_C(2048);
+  if (lgC == 12) {
+    if (abytes > 64u * 1024u) return hipErrorInvalidValue;
+    DLSM_MUNP_C(4096);
+  } else {
+    DLSM_MUNP_C(2048);
+  }
 #undef DLSM_MUNP_C
 #undef DLSM_MUNP
   return hipGetLastError();
 }
-
 
 hipError_t launch_version_route(const VersionDev& v, KeyDesc keys, uint64_t snapshot, uint64_t* slot_mask,
                                 uint32_t* level_file, uint32_t* hv, uint32_t* gl, hipStream_t s) {

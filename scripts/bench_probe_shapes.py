@@ -24,14 +24,18 @@ SHAPES = {
     "l0_plus_levels_16": [153_846] * 10 + [600_000, 1_600_000, 3_000_000, 153_846 * 4, 153_846 * 40, 2_000_000],
     "dedup_shifted_8": [1_600_000 - 97 * f for f in range(8)],
 }
+SHAPES["mixed_set"] = SHAPES["mixed_8"]  # bench.py SHAPE_LEGS names
+SHAPES["dedup_shifted"] = SHAPES["dedup_shifted_8"]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lookups", type=int, default=20_000_000)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--shapes", default="equal_8x1.6M,mixed_8,equal_8x153846,l0_plus_levels_16,dedup_shifted_8")
     ap.add_argument("--check", type=int, default=1_000_000, help="lookups checked against the oracle")
+    ap.add_argument("--paths", default="auto,per_group,direct",
+                    help="auto (one-pass multi-group), per_group (a pass per group), direct")
     args = ap.parse_args()
 
     import numpy as np
@@ -68,7 +72,7 @@ def main():
         rec = {"shape": name, "filters": F, "keys_per_filter": sizes, "lookups": Q}
         ref_mask = None
         for path, label, multi in ((0, "auto", 1), (0, "per_group", 0), (1, "direct", 1)):
-            if label == "per_group" and len(set(sizes)) == 1:
+            if label not in args.paths.split(",") or (label == "per_group" and len(set(sizes)) == 1):
                 continue
             ctx.set_path(path)
             ctx.set_option(dlsm_amd.OPT_PROBE_MULTI, multi)

@@ -22,7 +22,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
   i=$((i+1))
   mkdir -p "$OUT/pmc" &&
   timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc/p$i" -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-version --no-mixed $BARGS \
+    python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-version --no-mixed --no-block $BARGS \
     > "$OUT/pmc/p$i.json" 2> "$OUT/pmc/p$i.err" || exit 1
 done &&
 for grp in "FETCH_SIZE" "WRITE_SIZE"; do
@@ -32,10 +32,20 @@ for grp in "FETCH_SIZE" "WRITE_SIZE"; do
     python3 scripts/bench_version_probe.py --lookups 100000000 --check 0 --paths direct \
     > "$OUT/pmcv/p$i.json" 2> "$OUT/pmcv/p$i.err" || exit 1
 done &&
-python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" "$OUT/pmcv" > /dev/null &&
+for shape in mixed_set dedup_shifted; do
+  for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    mkdir -p "$OUT/pmc_$shape" &&
+    timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc_$shape/p$i" -o run -- \
+      python3 scripts/bench_probe_shapes.py --shapes $shape --lookups 100000000 --reps 3 --check 0 --paths auto \
+      > "$OUT/pmc_$shape/p$i.json" 2> "$OUT/pmc_$shape/p$i.err" || exit 1
+  done
+done &&
+python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" "$OUT/pmcv" \
+  mixed_set="$OUT/pmc_mixed_set" dedup_shifted="$OUT/pmc_dedup_shifted" > /dev/null &&
 timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-legacy --no-version --no-mixed \
+  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-legacy --no-version --no-mixed --no-block \
   --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
 python3 scripts/sampled_kernel_stats.py "$OUT/prof" 10 > "$OUT/sampled_kernel_stats.txt" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/vprof" -o run -- \

@@ -8,11 +8,14 @@ so it is doubled here; WRITE_SIZE is exact for 16-B-per-lane stores.  Both
 count Infinity-Cache hits as well (memory-side counters), so the figure is
 fabric traffic, an upper bound on HBM traffic.
 
-    python scripts/pmc_traffic.py PMC_DIR BENCH_JSON OUT_JSON [VERSION_PMC_DIR]
+    python scripts/pmc_traffic.py PMC_DIR BENCH_JSON OUT_JSON [VERSION_PMC_DIR] [NAME=SHAPE_PMC_DIR ...]
 
 VERSION_PMC_DIR: FETCH/WRITE passes of scripts/bench_version_probe.py (its
 version set-up builds 426 filters, so its launches are kept apart from the
-bench's build pass).
+bench's build pass).  NAME=SHAPE_PMC_DIR: FETCH/WRITE passes of
+scripts/bench_probe_shapes.py --paths auto over one of bench.py's SHAPE_LEGS
+(mixed_set, dedup_shifted): the one-pass probe's three kernels, one launch
+each per call (one slice launch per image-width class: one class in both).
 """
 import csv
 import glob
@@ -26,6 +29,7 @@ PASSES = {"probe": ("probe_partition_kernel", "probe_slice_kernel", "probe_unper
           "build": ("full_partition_kernel", "full_slice_kernel"),
           "legacy": ("legacy_partition_kernel", "legacy_slice_kernel"),
           "version": ("version_lds_kernel",)}
+SHAPE_KERNELS = ("probe_mpartition_kernel", "probe_slice_kernel", "probe_munpermute_kernel")
 
 
 def per_kernel(pmc_dir):
@@ -42,8 +46,13 @@ def main():
     pmc_dir, bench_json, out_json = sys.argv[1:4]
     bench = json.load(open(bench_json))
     vals = per_kernel(pmc_dir)
-    if len(sys.argv) > 4:  # the version probe's own passes
-        vv = per_kernel(sys.argv[4])
+    shapes = {}
+    for a in sys.argv[4:]:
+        if "=" in a:  # a probe-shape leg's own passes
+            name, d = a.split("=", 1)
+            shapes[name] = per_kernel(d)
+            continue
+        vv = per_kernel(a)  # the version probe's own passes
         if "version_lds_kernel" in vv:
             vals["version_lds_kernel"] = vv["version_lds_kernel"]
     out = {"source": pmc_dir, "config": {k: bench.get("config", bench).get(k) for k in
@@ -67,6 +76,18 @@ def main():
             continue
         out[name] = {"fetch_bytes": round(fetch), "write_bytes": round(write),
                      "traffic_bytes": round(fetch + write), "kernels": detail}
+    for name, sv in shapes.items():
+        detail = {}
+        for k in SHAPE_KERNELS:
+            if not sv.get(k):
+                continue
+            detail[k] = {"fetch_bytes": round(statistics.median(sv[k]["FETCH_SIZE"]) * 1024 * 2),
+                         "write_bytes": round(statistics.median(sv[k]["WRITE_SIZE"]) * 1024)}
+        if detail:
+            fetch = sum(d["fetch_bytes"] for d in detail.values())
+            write = sum(d["write_bytes"] for d in detail.values())
+            out[name] = {"fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
+                         "kernels": detail}
     json.dump(out, open(out_json, "w"), indent=1)
     print(json.dumps(out))
 

@@ -90,3 +90,50 @@ def test_config4_full_16x1p6m_batch(gpu, orc):
         assert int(L[s]) == len(want[s]) == 2_000_069
         assert got[: int(L[s])].tobytes() == want[s], s
         assert (got[int(L[s]):] == 0xEE).all()
+
+
+@pytest.mark.parametrize("shape", ["mixed_set", "dedup_shifted"])
+def test_realistic_filter_sets_full_100m_lookups(gpu, orc, shape):
+    """The bench's realistic probe legs (bench.py SHAPE_LEGS): the config-3
+    lookups against 8 filters of different line counts -- the one-pass
+    multi-group probe (round 6) -- every one of the 100 M mask bytes against
+    the oracle, and against the per-group passes (DLSM_OPT_PROBE_MULTI = 0)."""
+    import torch
+
+    import bench
+    import dlsm_amd
+    from dlsm_amd import workload as W
+
+    sizes = bench.SHAPE_LEGS[shape]
+    Fs = len(sizes)
+    tabs, outs = [], []
+    for f, n in enumerate(sizes):
+        v = torch.arange(n, device="cuda", dtype=torch.int64) * Fs + f
+        tabs.append(dlsm_amd.Keys(W.dbbench_keys_torch(v), n, 20))
+        outs.append(torch.zeros(dlsm_amd.full_size(n)[0], dtype=torch.uint8, device="cuda"))
+    lens = torch.zeros(Fs, dtype=torch.uint64, device="cuda")
+    torch.cuda.synchronize()
+    gpu.full_build_dev(tabs, outs, lens, 10)
+    gpu.sync()
+    del tabs
+    filters = [o[: int(n)] for o, n in zip(outs, lens.cpu().numpy())]
+    host_filters = [f.cpu().numpy().tobytes() for f in filters]
+    for f, n in enumerate(sizes):
+        assert host_filters[f] == orc.full_build(orc.dbbench_keys(f, Fs, n), n), f
+    qk = orc.keys_from_values(orc.mt_values(1000, 2 * F * N, Q))
+    fs = gpu.filterset(filters, on_device=True)
+    qd = torch.from_numpy(qk).cuda()
+    mask = torch.empty(Q, dtype=torch.uint8, device="cuda")
+    want = orc.full_probe(host_filters, qk, Q, nthreads=THREADS)
+    assert want.any()
+    for multi in (1, 0):
+        mask.fill_(0xEE)
+        torch.cuda.synchronize()
+        gpu.set_option(dlsm_amd.OPT_PROBE_MULTI, multi)
+        try:
+            gpu.full_probe_dev(fs, dlsm_amd.Keys(qd, Q, 20), mask)
+            gpu.sync()
+        finally:
+            gpu.set_option(dlsm_amd.OPT_PROBE_MULTI, 1)
+        assert np.array_equal(mask.cpu().numpy(), want), multi
+    fs.close()

@@ -187,3 +187,10 @@ def test_variable_length_keys(gpu, orc):
         assert want[::97].any()
     finally:
         fs.close()
+
+
+def test_group_with_256_slices(gpu, orc):
+    # 8 filters of 3.35 M keys: one byte-wide group of 65,430 lines = 256
+    # slices of 256 lines (the most a group may have), beside a packed single
+    sizes = [3_350_000] * 8 + [100_000]
+    _check(gpu, orc, _filters(orc, sizes), 400_001, 22)
