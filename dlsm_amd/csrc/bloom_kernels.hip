@@ -1176,6 +1176,15 @@ __device__ __forceinline__ uint32_t probe_entry(uint32_t h, uint32_t line_off) {
 __device__ __forceinline__ uint32_t probe_entry_off(uint32_t e) {
   return ((e >> 9) & 0xffu) | (((e >> 26) & 7u) << 8);
 }
+// One-pass multi-group entries: the probe's two 9-bit hash fields packed
+// low -- h mod 512 in bits [0, 9), rotr(h, 17) mod 512 (hash bits [17, 26))
+// in bits [9, 18) -- once per key, the line offset inside the slice (< 2^11)
+// in bits [18, 29): one shift-or per group in the partition.  The slice pass
+// reads only (x + q * (e >> 9)) mod 512, so the higher bits of either field
+// never matter; padding is 0 (line 0, answers never read).
+constexpr uint32_t kMGEntryOffShift = 18;
+constexpr uint32_t kMGPadEntry = 0u;
+__device__ __forceinline__ uint32_t mg_entry_hash(uint32_t h) { return (h & 0x1ffu) | ((h >> 8) & 0x3fe00u); }
 
 // f(b) for every bucket b < n (n <= kMaxSlices + 1): one bucket per thread
 // when the workgroup has enough threads.  A strided loop's per-lane trip
@@ -1477,9 +1486,9 @@ __global__ __launch_bounds__(NT, DLSM_PROBE_MINWAVES) void probe_slice_kernel(
             const uint32_t e4[4] = {hv[u].x, hv[u].y, hv[u].z, hv[u].w};
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-              xs[4 * u + j] = e4[j];
-              ds[4 * u + j] = e4[j] >> 17;  // low 9 bits of rotr(h, 17)
-              bs[4 * u + j] = LGW == 3 ? (e4[j] & ((R - 1u) << 9)) : probe_entry_off(e4[j]) * LB;
+              xs[4 * u + j] = e4[j];                       // bits [0, 9): h mod 512
+              ds[4 * u + j] = e4[j] >> 9;                  // bits [9, 18): rotr(h, 17) mod 512
+              bs[4 * u + j] = (e4[j] >> kMGEntryOffShift) * LB;  // the line's image bytes
               acc[4 * u + j] = WM;
             }
           }
@@ -1769,8 +1778,11 @@ __device__ __forceinline__ void hash_full_chunk(const KeyDesc& kd, uint64_t firs
 // the next set (two sets of histograms alternate); after the scatter.  The
 // slices are 2^lgR lines (a power of two in the one-pass layout), so a line's
 // slice and offset are a shift and a mask.
+#ifndef DLSM_MG_PWAVES
+#define DLSM_MG_PWAVES 5  // partition: waves per SIMD the register budget must allow (A/B knob; 4: no spill, 1-2 % slower)
+#endif
 template <int MODE, int NT, int C, int P>
-__global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const MGroupDev* __restrict__ groups,
+__global__ __launch_bounds__(NT, DLSM_MG_PWAVES) void probe_mpartition_kernel(KeyDesc kd, const MGroupDev* __restrict__ groups,
                                                               int G, uint32_t rowlen, uint32_t region,
                                                               uint32_t* __restrict__ entries,
                                                               uint16_t* __restrict__ pos,
@@ -1802,6 +1814,11 @@ __global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const 
   uint32_t* ereg = entries + static_cast<uint64_t>(c) * region;
   const uint32_t lane = tid & 63;
   const int wv = wave_id();
+  // the part of every group's entry that does not depend on the group
+  // (mg_entry): computed once per key
+  uint32_t hk[PER];
+#pragma unroll
+  for (int r = 0; r < PER; r++) hk[r] = mg_entry_hash(h[r]);
   for (int j0 = 0, q = 0; j0 < G; j0 += P, q ^= 1) {
     const int np = min(P, G - j0);  // groups in this set (uniform)
     uint32_t pk[P][PER], e[P][PER];   // (rank << 8) | slice; the entry
@@ -1816,7 +1833,7 @@ __global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const 
       for (int r = 0; r < PER; r++) {
         const uint32_t line = fastmod(h[r], L, magic);
         pk[pp][r] = line >> lgR;
-        e[pp][r] = probe_entry(h[r], line & (R - 1u));
+        e[pp][r] = hk[r] | ((line & (R - 1u)) << kMGEntryOffShift);
       }
       if (full) {
 #pragma unroll
@@ -1856,7 +1873,7 @@ __global__ __launch_bounds__(NT) void probe_mpartition_kernel(KeyDesc kd, const 
           trow[tcol + b] = static_cast<uint16_t>(eoff + run);
         }
         if (b < S)
-          for (uint32_t p = run + cnt[k]; p < run + pc[k]; p++) st[p] = kProbePadEntry;
+          for (uint32_t p = run + cnt[k]; p < run + pc[k]; p++) st[p] = kMGPadEntry;
         run += pc[k];
       }
       if (j0 + P < G) {
