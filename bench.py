@@ -444,6 +444,11 @@ def main():
     # ---- the sealed filter block, N=1: recorded ----
     if world == 1 and tables and not args.no_block:
         result["block"] = block_leg(ctx, stream, tables, bpk)
+        bt = load_traffic(args.traffic, result["config"], "block")
+        if bt:  # PMC fabric bytes of one sealed batch build (partition + slice + seal)
+            result["block"]["traffic"] = bt["traffic_bytes"]
+            result["block"]["traffic_alg_ratio"] = round(
+                bt["traffic_bytes"] / (result["block"]["alg_bytes_per_key"] * len(tables) * tables[0].n), 3)
 
     # ---- the read shapes a Version presents, N=1:
     # recorded beside `value` ----
@@ -1149,10 +1154,13 @@ def block_leg(ctx, stream, tables, bpk, reps=20):
     built as filter BLOCKS -- filter bytes + the 5-byte trailer (type byte +
     masked crc32c, table/table_builder_computeside.cc:418-428,
     util/crc32c.h:17-37) -- in one device-resident batch
-    (dlsm_bloom_full_build_block_dev: the build, then the crc passes), against
+    (dlsm_bloom_full_build_block_dev: the build's slice pass also computes
+    the crc32c register of each slice's lines from LDS, and one small seal
+    kernel folds a filter's slice registers and appends the trailer), against
     the plain batch build on the same stream, HIP events over `reps` calls
-    each.  Parity: tests/test_gpu_parity.py (trailers equal the reference
-    crc32c.cc goldens)."""
+    each.  Algorithmic bytes: 20 B key read + the block written once (the crc
+    reads the filter bytes from LDS, not HBM).  Parity: tests/test_gpu_block_seal.py, tests/test_gpu_parity.py
+    (trailers equal the reference crc32c.cc goldens)."""
     import torch
 
     import dlsm_amd
@@ -1177,9 +1185,12 @@ def block_leg(ctx, stream, tables, bpk, reps=20):
     block = timed(ctx.full_build_block_dev)
     L = lens.cpu().numpy()
     nk = sum(t.n for t in tables)
+    alg = nk * 20 + int(L.sum())
+    gbs = alg / (block * 1e-3) / 1e9
     rec = {"ms": round(block, 4), "build_ms": round(plain, 4),
            "crc_seal_ms": round(block - plain, 4), "crc_overhead_frac": round((block - plain) / plain, 4),
-           "tables": T, "block_bytes": int(L.sum()), "mkeys_s": round(nk / block / 1e3, 1)}
+           "tables": T, "block_bytes": int(L.sum()), "mkeys_s": round(nk / block / 1e3, 1),
+           "alg_GBs": round(gbs, 1), "alg_bytes_per_key": round(alg / nk, 3), "frac": round(gbs / HBM_PEAK_GBS, 4)}
     del outs, lens
     return rec
 

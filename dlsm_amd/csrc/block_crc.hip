@@ -225,6 +225,48 @@ hipError_t launch_crc_streams(const void* streams, int n, int max_parts, uint32_
 
 size_t crc_stream_size() { return sizeof(CrcStream); }
 
+// Host tables of the fused seal (bloom_internal.h kCrcTabWords): slice-by-4
+// tables, then powers x^(8n) mod P for the build slice's thread segments,
+// whole slices and whole lines.
+void full_block_crc_tables(int lgR, uint32_t* out) {
+  auto mul = [](uint32_t a, uint32_t b) {
+    uint32_t p = 0;
+    for (int i = 0; i < 32; i++) {
+      if (a & (0x80000000u >> i)) p ^= b;
+      b = (b & 1u) ? (b >> 1) ^ kCrcPoly : (b >> 1);
+    }
+    return p;
+  };
+  auto x8n = [&](uint64_t n) {  // x^(8n) by square-and-multiply
+    uint32_t r = 0x80000000u, sq = 0x00800000u;  // x^0, x^8
+    for (; n; n >>= 1, sq = mul(sq, sq))
+      if (n & 1u) r = mul(r, sq);
+    return r;
+  };
+  uint32_t* T = out;
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ kCrcPoly : (c >> 1);
+    T[i] = c;
+  }
+  for (int t = 1; t < 4; t++)
+    for (uint32_t i = 0; i < 256; i++) T[256 * t + i] = (T[256 * (t - 1) + i] >> 8) ^ T[T[256 * (t - 1) + i] & 0xffu];
+  const uint64_t R = 1ull << lgR;
+  const uint64_t seg = R * 64u / 512u;  // bytes per build-slice thread
+  uint32_t* PS = out + 1024;
+  const uint32_t step_s = x8n(seg);
+  PS[0] = 0x80000000u;
+  for (int m = 1; m < 512; m++) PS[m] = mul(PS[m - 1], step_s);
+  uint32_t* P1 = PS + 512;
+  const uint32_t step_1 = x8n(R * 64u);
+  P1[0] = 0x80000000u;
+  for (int m = 1; m < 256; m++) P1[m] = mul(P1[m - 1], step_1);
+  uint32_t* P64 = P1 + 256;
+  const uint32_t step_64 = x8n(64);
+  P64[0] = 0x80000000u;
+  for (int m = 1; m <= 2048; m++) P64[m] = mul(P64[m - 1], step_64);
+}
+
 void crc_stream_fill(void* dst, const uint8_t* data, const uint64_t* len_dev, uint64_t len_host,
                      uint32_t extra) {
   CrcStream* c = static_cast<CrcStream*>(dst);

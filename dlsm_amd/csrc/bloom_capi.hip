@@ -165,6 +165,10 @@ struct dlsm_ctx {
   // crc32c / block sealing
   DevBuf<uint8_t> crc_streams;
   DevBuf<uint32_t> crc_partial;
+  DevBuf<uint32_t> crc_tabs;  // fused seal: full_block_crc_tables(crc_tabs_lgr)
+  DevBuf<uint32_t> crc_cnt;   // fused seal: per-job slice counters (zero between calls)
+  int crc_tabs_lgr = -1;
+  uint64_t crc_tabs_gen = 0;
   DevBuf<uint8_t*> crc_outp;
   DevBuf<uint64_t> crc_cap;
   DevBuf<uint32_t> crc_val;
@@ -676,6 +680,8 @@ int dlsm_ctx_destroy(dlsm_ctx* ctx) {
   ctx->st_filter.release();
   ctx->crc_streams.release();
   ctx->crc_partial.release();
+  ctx->crc_tabs.release();
+  ctx->crc_cnt.release();
   ctx->crc_outp.release();
   ctx->crc_cap.release();
   ctx->crc_val.release();
@@ -885,7 +891,7 @@ int dlsm_ctx_stats(dlsm_ctx* ctx, uint64_t* device_allocs, uint64_t* device_byte
   add(ctx->lentries); add(ctx->ltab); add(ctx->pos); add(ctx->smask); add(ctx->hashes);
   add(ctx->vgl); add(ctx->vabyte); add(ctx->vplan);
   add(ctx->st_keys); add(ctx->st_offs); add(ctx->st_out); add(ctx->st_len); add(ctx->st_filter);
-  add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_outp); add(ctx->crc_cap);
+  add(ctx->crc_streams); add(ctx->crc_partial); add(ctx->crc_tabs); add(ctx->crc_cnt); add(ctx->crc_outp); add(ctx->crc_cap);
   add(ctx->crc_val); add(ctx->sel);
   if (device_allocs) *device_allocs = n;
   if (device_bytes) *device_bytes = b;
@@ -1052,8 +1058,12 @@ bool is_hash_set(const dlsm_keyset& k) {
   return k.offsets == nullptr && k.key_len == 4 && k.suffix_len == 0 && (k.n == 0 || aligned(k.bytes, 4));
 }
 
+// seal (dlsm_bloom_full_build_block_dev): on the sliced path the slices also
+// compute their crc32c partials and a seal kernel appends the block trailer
+// (*sealed = true); the direct path leaves sealing to the caller.
 int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, int bits_per_key,
-                        uint64_t* out_len_dev, bool hashed) {
+                        uint64_t* out_len_dev, bool hashed, bool seal = false, bool* sealed = nullptr) {
+  if (sealed) *sealed = false;
   if (!ctx || n_jobs < 0 || (n_jobs > 0 && (!jobs || !out_len_dev))) return DLSM_E_ARG;
   if (ctx->fault) return -ctx->fault;
   if (n_jobs == 0) return DLSM_OK;
@@ -1143,6 +1153,23 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
   if (sliced_ok) {
     DLSM_CHECK(ctx->entries.ensure(entry));
     DLSM_CHECK(ctx->tab.ensure(tabw));
+    uint32_t* crc_part = nullptr;
+    if (seal) {
+      DLSM_CHECK(ctx->crc_partial.ensure(slice));
+      if (ctx->crc_tabs_lgr != lgR || ctx->crc_tabs.gen != ctx->crc_tabs_gen) {
+        DLSM_CHECK(ctx->crc_tabs.ensure(kCrcTabWords));
+        std::vector<uint32_t> t(kCrcTabWords);
+        full_block_crc_tables(lgR, t.data());
+        DLSM_CHECK(ctx_upload(ctx, ctx->crc_tabs.p, t.data(), sizeof(uint32_t) * kCrcTabWords, s));
+        ctx->crc_tabs_lgr = lgR;
+        ctx->crc_tabs_gen = ctx->crc_tabs.gen;
+      }
+      crc_part = ctx->crc_partial.p;
+      if (ctx->crc_cnt.cap < static_cast<size_t>(n_jobs) || !ctx->crc_cnt.p) {
+        DLSM_CHECK(ctx->crc_cnt.ensure(n_jobs));
+        DLSM_TRY(hipMemsetAsync(ctx->crc_cnt.p, 0, sizeof(uint32_t) * ctx->crc_cnt.cap, s));  // reset by the sealers after
+      }
+    }
     // Job groups of about equal chunk counts: group g's partition (HBM-bound)
     // runs on the helper stream while the context stream runs group g-1's
     // slices (LDS-bound).
@@ -1169,7 +1196,12 @@ int full_build_dev_impl(dlsm_ctx* ctx, const dlsm_build_job* jobs, int n_jobs, i
       if (split) DLSM_CHECK(join_part(ctx));
       if (ng > 1) DLSM_CHECK(hand_over(ctx->aux, s, ctx->ev_part[g % kStageEvents]));
       DLSM_TRY(launch_full_slices(ctx->jobs.p, slice0s, n_jobs, s0, slice_at(cut[g + 1]) - s0,
-                                  ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, s));
+                                  ctx->dchunk.p, ctx->entries.p, ctx->tab.p, lgR, s, crc_part,
+                                  ctx->crc_tabs.p, ctx->crc_cnt.p));
+    }
+    if (seal) {
+      DLSM_TRY(launch_full_block_seal(ctx->jobs.p, n_jobs, crc_part, ctx->crc_tabs.p, lgR, s));
+      if (sealed) *sealed = true;
     }
   } else {
     DLSM_TRY(launch_full_count(ctx->jobs.p, chunk0s, n_jobs, chunk, ctx->dchunk.p, mode, s));
@@ -1428,7 +1460,11 @@ int dlsm_bloom_full_build_block_dev(dlsm_ctx* ctx, const dlsm_build_job* jobs, i
     caps[j] = jobs[j].out_cap;
     max_total = std::max(max_total, full_filter_len(jobs[j].keys.n, bits_per_key) + 1);
   }
-  DLSM_CHECK(dlsm_bloom_full_build_dev(ctx, fj.data(), n_jobs, bits_per_key, out_len_dev));
+  // the sliced build seals its own filters (the crc fused into its slice
+  // pass); the direct path takes the separate crc passes below
+  bool sealed = false;
+  DLSM_CHECK(full_build_dev_impl(ctx, fj.data(), n_jobs, bits_per_key, out_len_dev, false, true, &sealed));
+  if (sealed) return DLSM_OK;
   std::vector<std::vector<uint8_t>> st(n_jobs, std::vector<uint8_t>(crc_stream_size()));
   for (int j = 0; j < n_jobs; j++) crc_stream_fill(st[j].data(), jobs[j].out, out_len_dev + j, 0, 1);
   return run_crc(ctx, st, n_jobs, max_total, outs.data(), caps.data(), out_len_dev, nullptr);

@@ -200,9 +200,23 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
                                  uint32_t chunk_first, uint32_t n_chunks, uint32_t* dchunk,
                                  uint32_t* entries, uint16_t* tab, int lgR, int mode, bool exact,
                                  hipStream_t s);
+// crc_part (or nullptr): each slice's crc32c register contribution, for
+// launch_full_block_seal; crc_tabs: full_block_crc_tables(lgR).
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
-                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s);
+                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s,
+                              uint32_t* crc_part = nullptr, const uint32_t* crc_tabs = nullptr,
+                              uint32_t* crc_cnt = nullptr);  // per-job counters, zero between calls
+// Seal each job's filter as a filter block (after its sliced build with
+// crc_part): [filter][type 0][masked crc32c], out_len += 5.
+hipError_t launch_full_block_seal(const FullJobDev* jobs, int n_jobs, const uint32_t* crc_part,
+                                  const uint32_t* crc_tabs, int lgR, hipStream_t s);
+// Host tables for the fused seal at slices of 2^lgR lines (u32): the
+// slice-by-4 crc32c tables (1024), per build-slice thread t x^(8 * 2^lgR / 8 *
+// (511 - t)) (512), x^(8 * 2^lgR * 64 * m) for m < 256, x^(8 * 64 * m) for
+// m <= 2^11.
+constexpr size_t kCrcTabWords = 1024 + 512 + 256 + 2049;
+void full_block_crc_tables(int lgR, uint32_t* out);
 
 hipError_t launch_probe_direct(const FilterDev* fs, int n_filters, KeyDesc keys, uint8_t* mask,
                                int mode, hipStream_t s);

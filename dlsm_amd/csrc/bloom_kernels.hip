@@ -215,6 +215,16 @@ __device__ __forceinline__ void write_trailer(uint8_t* out, uint32_t L, int k) {
 // 5 dwords: conflict-free).  GENERIC: each thread hashes its keys directly.
 // ---------------------------------------------------------------------------
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// A 16-byte store through a global-address-space pointer.  Output pointers
+// read from a job descriptor are generic, and generic (flat) stores count in
+// lgkmcnt as well as vmcnt: the next LDS wait then waits for the stores to
+// complete (the slice passes' LDS -> HBM loops serialised on store latency).
+typedef __attribute__((address_space(1))) u32x4 g_u32x4_w;
+__device__ __forceinline__ void st_global16(void* p, uint4 v) {
+  *(g_u32x4_w*)(reinterpret_cast<uintptr_t>(p)) = u32x4{v.x, v.y, v.z, v.w};
+}
+typedef __attribute__((address_space(1))) uint8_t g_u8_w;
+__device__ __forceinline__ void st_global1(void* p, uint8_t v) { *(g_u8_w*)(reinterpret_cast<uintptr_t>(p)) = v; }
 
 template <int NT, int KPT, int KB = 20>
 struct K20Tile {
@@ -903,7 +913,119 @@ __device__ __forceinline__ uint64_t job_distinct(const FullJobDev& J, const uint
 // entries in flight per lane), ORs bits with ds_or, and the slice streams out
 // with 16-byte stores.
 // ---------------------------------------------------------------------------
-constexpr int kSliceBlock = 512;        // build slices (32 KiB LDS -> 4 per CU)
+constexpr int kSliceBlock = 512;
+
+// ---- crc32c of a filter slice (sealed blocks, round 6) --------------------
+// Reflected Castagnoli arithmetic as in block_crc.hip: the register after
+// bytes A||B is reg(A) * x^(8|B|) xor raw(B) (raw: the register run from 0),
+// and leading zero bytes leave a zero register unchanged.  A slice of nl
+// lines (nl * 64 bytes) is front-padded with zeros to R * 64 bytes; thread t
+// runs the table CRC over its 16 * R / 512 words (the filter's first byte
+// seeds the register with 0xffffffff, crc32c's initial value), and its
+// register, times x^(8 * bytes after its segment) from a host table, is
+// XOR-reduced over the workgroup.
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    p ^= (a & (0x80000000u >> i)) ? b : 0u;
+    b = (b >> 1) ^ ((b & 1u) ? 0x82f63b78u : 0u);
+  }
+  return p;
+}
+#ifndef DLSM_CRC_NIB
+#define DLSM_CRC_NIB 1  // slice CRC by 4-bit tables (8 conflict-free lookups / word) instead of byte tables
+#endif
+__device__ __forceinline__ uint32_t crc_word(uint32_t r, uint32_t w, const uint32_t* T) {
+  r ^= w;
+  if constexpr (DLSM_CRC_NIB) {
+    // T: 8 tables of 16 (nibble q of the register): 16 entries in 16 banks,
+    // so a lookup instruction never conflicts (random byte tables: ~3.5-way)
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) x ^= T[16 * q + ((r >> (4 * q)) & 15u)];
+    return x;
+  } else {
+    return T[768 + (r & 0xffu)] ^ T[512 + ((r >> 8) & 0xffu)] ^ T[256 + ((r >> 16) & 0xffu)] ^ T[r >> 24];
+  }
+}
+template <uint32_t R>
+__device__ __forceinline__ uint32_t crc_slice_partial(const uint32_t* sl, uint32_t nl, bool seed,
+                                                      const uint32_t* T, uint32_t shift, uint32_t* wsum) {
+  constexpr uint32_t WPT = R * 16u / kSliceBlock;  // words per thread (multiple of 4: R >= 128)
+  static_assert(WPT % 4 == 0, "whole 16-byte reads");
+  const uint32_t tid = threadIdx.x;
+  const uint32_t padw = (R - nl) * 16u;  // zero words in front (a multiple of 16)
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < WPT / 4; q++) {
+    const uint32_t i = tid * WPT + 4u * q;  // first word of this 16-byte piece (padded numbering)
+    if (i >= padw) {
+      const uint4 v = *reinterpret_cast<const uint4*>(sl + (i - padw));
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      if (seed && i == padw) r = 0xffffffffu;  // the filter's first byte: crc32c's initial register
+#pragma unroll
+      for (int j = 0; j < 4; j++) r = crc_word(r, w4[j], T);
+    }
+  }
+  r = crc_mulmod(r, shift);  // x^(8 * WPT * 4 * (threads after this one)), loaded at kernel start
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) r ^= __shfl_xor(r, d, 64);
+  __syncthreads();  // wsum is free (the walk and job_distinct are done)
+  if ((tid & 63) == 0) wsum[tid >> 6] = r;
+  __syncthreads();
+  uint32_t t = 0;
+#pragma unroll
+  for (int w = 0; w < kSliceBlock / 64; w++) t ^= wsum[w];
+  return t;
+}
+
+#ifndef DLSM_SEAL_LAST
+#define DLSM_SEAL_LAST 0  // 1: the last slice workgroup of a job seals it (0: a seal kernel launch)
+#endif
+// The crc32c register after a filter's L lines from its slices' partials
+// (slice s's register times x^(8 * bytes of the slices after it): P1 for
+// whole slices, P64 for the last slice's lines); the workgroup's threads fold
+// a slice each.  Partials are read with agent-scope loads (other XCDs wrote
+// them).  The result is meaningful in thread 0.
+template <uint32_t R>
+__device__ __forceinline__ uint32_t crc_seal_fold(const uint32_t* part, uint32_t L, const uint32_t* crc_tabs,
+                                                  uint32_t* wsum) {
+  const uint32_t S = (L + R - 1u) / R;  // slices holding bytes
+  const uint32_t* P1 = crc_tabs + 1024 + kSliceBlock;
+  const uint32_t* P64 = P1 + 256;
+  uint32_t x = 0;
+  for (uint32_t t = threadIdx.x; t + 1u < S; t += kSliceBlock)
+    x ^= crc_mulmod(__hip_atomic_load(part + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), P1[S - 2u - t]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x ^= __shfl_xor(x, d, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x != 0) return 0;
+  x = 0;
+#pragma unroll
+  for (int w = 0; w < kSliceBlock / 64; w++) x ^= wsum[w];
+  if (S == 0) return 0xffffffffu;  // no lines: the trailer's first byte starts the crc
+  return crc_mulmod(x, P64[L - (S - 1u) * R]) ^
+         __hip_atomic_load(part + (S - 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Run the register through the trailer (k, Fixed32 L) and the type byte (0);
+// append [type 0][crc32c::Mask(value)] at `t` (table/table_builder_computeside.cc:418-428).
+__device__ __forceinline__ void crc_seal_append(uint8_t* t, uint32_t r, uint32_t L, int k, const uint32_t* T) {
+  const uint8_t tail[6] = {static_cast<uint8_t>(static_cast<int8_t>(k)), static_cast<uint8_t>(L),
+                           static_cast<uint8_t>(L >> 8), static_cast<uint8_t>(L >> 16),
+                           static_cast<uint8_t>(L >> 24), 0u};
+#pragma unroll
+  for (int b = 0; b < 6; b++) r = (r >> 8) ^ T[(r ^ tail[b]) & 0xffu];
+  const uint32_t value = ~r;
+  const uint32_t m = ((value >> 15) | (value << 17)) + 0xa282ead8u;  // crc32c::Mask
+  t[0] = 0;  // kNoCompression
+  t[1] = static_cast<uint8_t>(m);
+  t[2] = static_cast<uint8_t>(m >> 8);
+  t[3] = static_cast<uint8_t>(m >> 16);
+  t[4] = static_cast<uint8_t>(m >> 24);
+}        // build slices (32 KiB LDS -> 4 per CU)
 // probe slices: 64 KiB LDS per workgroup, 512 or 1024 threads (launch_probe_slices)
 #ifndef DLSM_BUILD_WALKU
 #define DLSM_BUILD_WALKU 8
@@ -936,22 +1058,65 @@ constexpr int kWalkU = DLSM_BUILD_WALKU;  // hashes in flight per lane (build se
 constexpr int kProbeWalkU = DLSM_PROBE_U;    // probe walk, 64 KiB slices: unit windows in flight per wave
 constexpr int kProbeWalkU8 = DLSM_PROBE_U8;  // probe walk, 128 KiB slices
 
-template <int LGR>
+// Publish a slice's crc partial at agent scope and count the slice in its
+// job's counter (thread 0); *last = 1 in the workgroup whose count completes
+// the job.  The caller's next barrier makes *last visible.
+[[maybe_unused]] __device__ __forceinline__ void publish_slice_crc(uint32_t* part_slot, uint32_t part, uint32_t* cnt,
+                                                  uint32_t n_slices, uint32_t* last) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(part_slot, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    *last = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == n_slices ? 1u : 0u;
+  }
+}
+
+// CRC: the sealed filter block: once its lines
+// are in LDS, the slice also computes the crc32c register contribution of its
+// bytes (crc_slice_partial) into crc_part[slice]; full_block_seal_kernel folds
+// a filter's partials, runs them through the trailer and the type byte, and
+// appends [type 0][masked crc] -- no second pass over the filter bytes.
+// Measured (profiles/r06_block_seal_ab.txt): the slice pass 50 -> 65-69 us
+// for the bench's 16 x 2 MB filters plus a 5 us seal launch; sealing in the
+// last slice workgroup of each filter instead (DLSM_SEAL_LAST=1: agent-scope
+// partials, a release fence and a counter) costs more, 85-93 us, the fences.
+template <int LGR, bool CRC = false>
 __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     const FullJobDev* __restrict__ jobs, const uint32_t* __restrict__ slice0s, int n_jobs,
     const uint32_t* __restrict__ dchunk, const uint32_t* __restrict__ entries,
-    const uint16_t* __restrict__ tab, uint32_t block0) {
+    const uint16_t* __restrict__ tab, uint32_t block0, uint32_t* __restrict__ crc_part = nullptr,
+    const uint32_t* __restrict__ crc_tabs = nullptr, uint32_t* __restrict__ crc_cnt = nullptr) {
   constexpr uint32_t R = 1u << LGR;
   constexpr int NW = kSliceBlock / 64;
   __shared__ __attribute__((aligned(16))) uint32_t sl[R * 16];
   __shared__ uint32_t wsum[NW];
   __shared__ uint32_t walk_scr[NW * kWalkScratch];
+  // crc32c tables (nibble: 512 B; 4 KiB more LDS would cost a workgroup per CU)
+  __shared__ uint32_t crcT[CRC ? (DLSM_CRC_NIB ? 128 : 1024) : 1];
   __shared__ int sj;
+  __shared__ uint32_t s_last;  // CRC: this workgroup completed its job's slice count
   const int tid = threadIdx.x;
   const int wv = wave_id();  // wave-uniform (SGPR): keeps the segment walk's control flow scalar
   const uint32_t bid = xcd_block(blockIdx.x, gridDim.x) + block0;  // slice index over all jobs
   if (tid == 0) sj = find_job(slice0s, n_jobs, bid);
+  // CRC: this thread's shift multiplier, loaded beside the tables and waited
+  // for before the first barrier, so that no wait for it after the filter
+  // stores also waits for those stores (vmcnt counts loads and stores in order)
+  uint32_t crc_shift = 0;
+  if constexpr (CRC) crc_shift = crc_tabs[1024 + kSliceBlock - 1 - tid];
   for (uint32_t w = tid; w < R * 16; w += kSliceBlock) sl[w] = 0;
+  if constexpr (CRC) {
+    if constexpr (DLSM_CRC_NIB) {
+      // nibble table q (byte q / 2 of the register, low or high half) from
+      // the byte table the slice-by-4 step uses for that byte (linear in it)
+      if (tid < 128u) {
+        const uint32_t q = tid >> 4, v = tid & 15u;
+        crcT[tid] = crc_tabs[(3u - (q >> 1)) * 256u + (v << (4u * (q & 1u)))];
+      }
+    } else {
+      for (uint32_t w = tid; w < 1024u; w += kSliceBlock) crcT[w] = crc_tabs[w];
+    }
+    asm volatile("" : "+v"(crc_shift));
+  }
   __syncthreads();
   const FullJobDev J = jobs[sj];
   const uint32_t s = bid - J.slice0;
@@ -964,6 +1129,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     return;
   }
   const uint32_t lo_line = s << LGR;
+  uint32_t part = 0;  // CRC: this slice's register contribution (0: no bytes past a lowered L)
   if (L != 0 && lo_line < L) {
     const uint32_t magic = fastmod_magic(L);
     if (L == J.L_spec || J.exact) {  // the partition bucketed by this L
@@ -1012,14 +1178,86 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
     }
     __syncthreads();
     const uint32_t nl = min(R, L - lo_line);
+    // CRC + DLSM_SEAL_LAST: the partial is published before the filter
+    // stores, so that the release fence does not wait for them to drain
+    constexpr bool early = CRC && DLSM_SEAL_LAST;
+    if constexpr (early) part = crc_slice_partial<R>(sl, nl, s == 0, crcT, crc_shift, wsum);
+    if constexpr (early) publish_slice_crc(crc_part + bid, part, crc_cnt + sj, J.n_slices, &s_last);
     uint4* dst = reinterpret_cast<uint4*>(J.out + static_cast<uint64_t>(lo_line) * 64u);
     const uint4* src = reinterpret_cast<const uint4*>(sl);
-    for (uint32_t w = tid; w < nl * 4u; w += kSliceBlock) dst[w] = src[w];
+    for (uint32_t w = tid; w < nl * 4u; w += kSliceBlock) st_global16(dst + w, src[w]);
+    if constexpr (CRC && !early) part = crc_slice_partial<R>(sl, nl, s == 0, crcT, crc_shift, wsum);
+  } else if constexpr (CRC && DLSM_SEAL_LAST) {
+    publish_slice_crc(crc_part + bid, 0u, crc_cnt + sj, J.n_slices, &s_last);  // no bytes past a lowered L
+  }
+  if constexpr (CRC) {
+#if DLSM_SEAL_LAST
+    // The job's last slice workgroup to finish seals the filter (no seal
+    // launch): every slice publishes its partial at agent scope, then counts
+    // itself in the job's counter (publish_slice_crc, before its filter
+    // stores); the one that completes the count reads the partials back
+    // (agent-scope loads after an acquire fence), writes the trailer, the
+    // block trailer and the length, and resets the counter for the next call.
+    // Only the sealer writes the trailer bytes and out_len.
+    __syncthreads();
+    if (s_last) {
+      __threadfence();
+      const uint32_t r = crc_seal_fold<R>(crc_part + J.slice0, L, crc_tabs, wsum);
+      if (tid == 0) {
+        write_trailer(J.out, L, J.k);
+        crc_seal_append(J.out + len, r, L, J.k, crc_tabs);
+        *J.out_len = len + 5u;
+        crc_cnt[sj] = 0;
+      }
+    }
+    return;
+#else
+    if (tid == 0) crc_part[bid] = part;
+#endif
   }
   if (s == 0 && tid == 0) {
     write_trailer(J.out, L, J.k);
     *J.out_len = len;
   }
+}
+
+// Seal every filter of a sliced batch build (CRC slices): one workgroup per
+// job folds its slices' partials -- slice s's register times x^(8 * bytes of
+// the slices after it) from the host tables (P1: whole slices, P64: whole
+// lines of the last slice) -- then runs the register through the 5-byte
+// trailer and the type byte (0), and appends [type][crc32c::Mask(value)]
+// (table/table_builder_computeside.cc:418-428): out_len += 5.  A job whose
+// build failed (out_len 0) is left alone.
+template <int LGR>
+__global__ __launch_bounds__(256) void full_block_seal_kernel(const FullJobDev* __restrict__ jobs,
+                                                              const uint32_t* __restrict__ crc_part,
+                                                              const uint32_t* __restrict__ crc_tabs) {
+  constexpr uint32_t R = 1u << LGR;
+  __shared__ uint32_t wx[4];
+  const FullJobDev J = jobs[blockIdx.x];
+  const uint64_t len = *J.out_len;  // L * 64 + 5 (slice 0 wrote it), or 0
+  if (len == 0) return;
+  const uint32_t L = static_cast<uint32_t>((len - 5u) / 64u);
+  const uint32_t S = (L + R - 1u) / R;  // slices holding bytes (a lowered L uses fewer)
+  const uint32_t* T = crc_tabs;
+  const uint32_t* P1 = crc_tabs + 1024 + kSliceBlock;  // x^(8 * R * 64 * m)
+  const uint32_t* P64 = P1 + 256;                     // x^(8 * 64 * m)
+  const uint32_t* part = crc_part + J.slice0;
+  uint32_t x = 0;  // slices 0 .. S-2, each shifted to the end of slice S-2
+  for (uint32_t t = threadIdx.x; t + 1u < S; t += 256u) x ^= crc_mulmod(part[t], P1[S - 2u - t]);
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x ^= __shfl_xor(x, d, 64);
+  if ((threadIdx.x & 63) == 0) wx[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  x = wx[0] ^ wx[1] ^ wx[2] ^ wx[3];
+  uint32_t r = 0xffffffffu;  // no lines (an empty filter): the trailer's first byte starts the crc
+  if (S != 0) {
+    const uint32_t nl_last = L - (S - 1u) * R;
+    r = crc_mulmod(x, P64[nl_last]) ^ part[S - 1u];  // after the last slice's lines
+  }
+  crc_seal_append(J.out + len, r, L, J.k, T);
+  *J.out_len = len + 5u;
 }
 
 // ---------------------------------------------------------------------------
@@ -2980,10 +3218,10 @@ __global__ __launch_bounds__(kLegacySliceBlock) void legacy_slice_kernel(
   if ((reinterpret_cast<uintptr_t>(J.out) & 15u) == 0) {
     const uint32_t nv = static_cast<uint32_t>(nb >> 4);
     for (uint32_t w = tid; w < nv; w += kLegacySliceBlock)
-      reinterpret_cast<uint4*>(dst)[w] = reinterpret_cast<const uint4*>(src)[w];
-    for (uint32_t i = nv * 16u + tid; i < nb; i += kLegacySliceBlock) dst[i] = src[i];
+      st_global16(reinterpret_cast<uint4*>(dst) + w, reinterpret_cast<const uint4*>(src)[w]);
+    for (uint32_t i = nv * 16u + tid; i < nb; i += kLegacySliceBlock) st_global1(dst + i, src[i]);
   } else {
-    for (uint32_t i = tid; i < nb; i += kLegacySliceBlock) dst[i] = src[i];
+    for (uint32_t i = tid; i < nb; i += kLegacySliceBlock) st_global1(dst + i, src[i]);
   }
   if (s == 0 && tid == 0) {
     J.out[bytes] = static_cast<uint8_t>(static_cast<int8_t>(J.k));  // dst->append(&hash_num, 1)
@@ -3061,31 +3299,40 @@ hipError_t launch_full_partition(const FullJobDev* jobs, const uint32_t* chunk0s
 
 hipError_t launch_full_slices(const FullJobDev* jobs, const uint32_t* slice0s, int n_jobs,
                               uint32_t slice_first, uint32_t n_slices, const uint32_t* dchunk,
-                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s) {
+                              const uint32_t* entries, const uint16_t* tab, int lgR, hipStream_t s,
+                              uint32_t* crc_part, const uint32_t* crc_tabs, uint32_t* crc_cnt) {
   if (n_slices == 0) return hipSuccess;
+#define DLSM_FSL(LG)                                                                                          \
+  do {                                                                                                        \
+    if (crc_part)                                                                                             \
+      full_slice_kernel<LG, true><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab, \
+                                                                   slice_first, crc_part, crc_tabs, crc_cnt);\
+    else                                                                                                      \
+      full_slice_kernel<LG, false><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries,     \
+                                                                    tab, slice_first);                       \
+  } while (0)
   switch (lgR) {
-    case 7:
-      full_slice_kernel<7><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
-                                                            slice_first);
-      break;
-    case 8:
-      full_slice_kernel<8><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
-                                                            slice_first);
-      break;
-    case 9:
-      full_slice_kernel<9><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
-                                                            slice_first);
-      break;
-    case 10:
-      full_slice_kernel<10><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
-                                                             slice_first);
-      break;
-    case 11:
-      full_slice_kernel<11><<<n_slices, kSliceBlock, 0, s>>>(jobs, slice0s, n_jobs, dchunk, entries, tab,
-                                                             slice_first);
-      break;
-    default:
-      return hipErrorInvalidValue;
+    case 7: DLSM_FSL(7); break;
+    case 8: DLSM_FSL(8); break;
+    case 9: DLSM_FSL(9); break;
+    case 10: DLSM_FSL(10); break;
+    case 11: DLSM_FSL(11); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef DLSM_FSL
+  return hipGetLastError();
+}
+
+hipError_t launch_full_block_seal(const FullJobDev* jobs, int n_jobs, const uint32_t* crc_part,
+                                  const uint32_t* crc_tabs, int lgR, hipStream_t s) {
+  if (n_jobs == 0 || DLSM_SEAL_LAST) return hipSuccess;  // the slices sealed the filters
+  switch (lgR) {
+    case 7: full_block_seal_kernel<7><<<n_jobs, 256, 0, s>>>(jobs, crc_part, crc_tabs); break;
+    case 8: full_block_seal_kernel<8><<<n_jobs, 256, 0, s>>>(jobs, crc_part, crc_tabs); break;
+    case 9: full_block_seal_kernel<9><<<n_jobs, 256, 0, s>>>(jobs, crc_part, crc_tabs); break;
+    case 10: full_block_seal_kernel<10><<<n_jobs, 256, 0, s>>>(jobs, crc_part, crc_tabs); break;
+    case 11: full_block_seal_kernel<11><<<n_jobs, 256, 0, s>>>(jobs, crc_part, crc_tabs); break;
+    default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

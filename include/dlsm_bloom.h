@@ -191,11 +191,13 @@ int dlsm_ctx_set_path(dlsm_ctx* ctx, int path);
  *   DLSM_OPT_FAULT_INJECT     test hook: v > 0 makes every build and probe call on the
  *                             context return -v (4 = DLSM_E_DEVICE, 5 = DLSM_E_NOMEM)
  *                             before touching the device; 0 (default) off
- *   DLSM_OPT_VERSION_SLICE_BYTES  dlsm_version_create on this context: a level >= 1 whose
+ *   DLSM_OPT_VERSION_SLICE_BYTES  EXPERIMENTAL (off by default, kept with its tests):
+ *                             dlsm_version_create on this context: a level >= 1 whose
  *                             filters hold more bytes goes to the sliced version probe
  *                             (0: $DLSM_VERSION_SLICE_MIN_BYTES, default never --
  *                             the sliced probe measured slower at 125 MB and 1.25 GB
- *                             levels; UINT64_MAX: never)
+ *                             levels, no size tried favours it; DESIGN.md §9 item 9
+ *                             names the form left to try; UINT64_MAX: never)
  *   DLSM_OPT_VERSION_PASS_SLICES  128 KiB slices per partition pass of the sliced version
  *                             probe, 1..1024 (default 1024; larger levels take several)
  *   DLSM_OPT_PROBE_MULTI      a filter set of several (L, k) groups (a Version's files of

@@ -42,8 +42,15 @@ for shape in mixed_set dedup_shifted; do
       > "$OUT/pmc_$shape/p$i.json" 2> "$OUT/pmc_$shape/p$i.err" || exit 1
   done
 done &&
+for grp in "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  mkdir -p "$OUT/pmc_block" &&
+  timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/pmc_block/p$i" -o run -- \
+    python3 scripts/bench_block.py --only-block --reps 3 \
+    > "$OUT/pmc_block/p$i.json" 2> "$OUT/pmc_block/p$i.err" || exit 1
+done &&
 python3 scripts/pmc_traffic.py "$OUT/pmc" "$OUT/pmc/p1.json" "$OUT/traffic.json" "$OUT/pmcv" \
-  mixed_set="$OUT/pmc_mixed_set" dedup_shifted="$OUT/pmc_dedup_shifted" > /dev/null &&
+  mixed_set="$OUT/pmc_mixed_set" dedup_shifted="$OUT/pmc_dedup_shifted" block="$OUT/pmc_block" > /dev/null &&
 timeout -k 10 400 python bench.py --traffic "$OUT/traffic.json" $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
   python3 bench.py --steps 10 --warmup 2 --no-cpu --no-e2e --no-legacy --no-version --no-mixed --no-block \

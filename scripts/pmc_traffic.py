@@ -15,7 +15,8 @@ version set-up builds 426 filters, so its launches are kept apart from the
 bench's build pass).  NAME=SHAPE_PMC_DIR: FETCH/WRITE passes of
 scripts/bench_probe_shapes.py --paths auto over one of bench.py's SHAPE_LEGS
 (mixed_set, dedup_shifted): the one-pass probe's three kernels, one launch
-each per call (one slice launch per image-width class: one class in both).
+each per call (one slice launch per image-width class: one class in both);
+block=DIR: passes of scripts/bench_block.py --only-block.
 """
 import csv
 import glob
@@ -30,6 +31,9 @@ PASSES = {"probe": ("probe_partition_kernel", "probe_slice_kernel", "probe_unper
           "legacy": ("legacy_partition_kernel", "legacy_slice_kernel"),
           "version": ("version_lds_kernel",)}
 SHAPE_KERNELS = ("probe_mpartition_kernel", "probe_slice_kernel", "probe_munpermute_kernel")
+# block=DIR: FETCH/WRITE passes of scripts/bench_block.py --only-block (the
+# sealed build: partition, slice pass with the crc fused, seal kernel if any)
+NAMED_KERNELS = {"block": ("full_partition_kernel", "full_slice_kernel", "full_block_seal_kernel")}
 
 
 def per_kernel(pmc_dir):
@@ -78,7 +82,7 @@ def main():
                      "traffic_bytes": round(fetch + write), "kernels": detail}
     for name, sv in shapes.items():
         detail = {}
-        for k in SHAPE_KERNELS:
+        for k in NAMED_KERNELS.get(name, SHAPE_KERNELS):
             if not sv.get(k):
                 continue
             detail[k] = {"fetch_bytes": round(statistics.median(sv[k]["FETCH_SIZE"]) * 1024 * 2),
