@@ -1980,20 +1980,49 @@ int probe_multi(dlsm_ctx* ctx, const dlsm_filterset* fs, const KeyDesc& kd, int 
   const int G = fs->mg_n;
   const int lgC = mg_chunk_lg(G);
   const uint64_t C = 1ull << lgC;
-  const uint64_t nC = (n + C - 1) >> lgC;
   const uint32_t rowlen = fs->mg_slices + static_cast<uint32_t>(G);
-  DLSM_CHECK(ctx->entries.ensure(nC * fs->mg_region));
-  DLSM_CHECK(ctx->smask.ensure(nC * fs->mg_abytes));
-  DLSM_CHECK(ctx->pos.ensure(nC * G * C));
-  DLSM_CHECK(ctx->tab.ensure(nC * rowlen));
-  DLSM_TRY(launch_probe_mpartition(kd, fs->d_mg, G, rowlen, fs->mg_region, fs->mg_stage_bytes, ctx->entries.p,
-                                   ctx->pos.p, ctx->tab.p, mode, s));
-  for (const MGClass& cl : fs->mg_classes)
-    DLSM_TRY(launch_probe_mslices(cl.lgw, cl.K, fs->d_mg, G, cl.s0, cl.S, rowlen, fs->mg_region, fs->mg_abytes,
-                                  static_cast<uint32_t>(nC), ctx->entries.p, ctx->tab.p, ctx->smask.p,
-                                  fs->d_mgplan + cl.plan_off, cl.wgs, s));
-  DLSM_TRY(launch_probe_munpermute(n, fs->d_mg, G, fs->mg_abytes, ctx->pos.p, ctx->smask.p, mask_dev,
-                                   (fs->F + 7) / 8, s));
+  const uint64_t mbytes = (fs->F + 7) / 8;
+  // Rounds of probe_round keys (DLSM_OPT_PROBE_ROUND_KEYS), pipelined over
+  // two streams as in the one-group path: round r's partition (HBM-bound, on
+  // the helper stream) beside round r-1's slice pass (LDS-bound) and
+  // unpermute, over kProbeBufs rotating buffer sets.
+  uint64_t round = n;
+  if (ctx->probe_round && ctx->probe_round < n) round = std::max<uint64_t>(C, (ctx->probe_round / C) * C);
+  const uint64_t n_rounds = (n + round - 1) / round;
+  const bool pipe = n_rounds > 1 && !ctx->probe_serial;
+  const int nbuf = pipe ? kProbeBufs : 1;
+  const uint64_t nCmax = (std::min(round, n) + C - 1) >> lgC;
+  const uint64_t estride = nCmax * fs->mg_region, astride = nCmax * fs->mg_abytes;
+  const uint64_t pstride = nCmax * G * C, tstride = nCmax * rowlen;
+  DLSM_CHECK(ctx->entries.ensure(estride * nbuf));
+  DLSM_CHECK(ctx->smask.ensure(astride * nbuf));
+  DLSM_CHECK(ctx->pos.ensure(pstride * nbuf));
+  DLSM_CHECK(ctx->tab.ensure(tstride * nbuf));
+  if (pipe) DLSM_CHECK(fork_aux(ctx));
+  hipStream_t ps = pipe ? ctx->aux : s;
+  for (uint64_t r = 0; r < n_rounds; r++) {
+    const uint64_t r0 = r * round;
+    const uint64_t nr = std::min(round, n - r0);
+    const uint64_t nC = (nr + C - 1) >> lgC;
+    const int b = static_cast<int>(r % nbuf);
+    uint32_t* ent = ctx->entries.p + b * estride;
+    uint8_t* ans = ctx->smask.p + b * astride;
+    uint16_t* pos = ctx->pos.p + b * pstride;
+    uint16_t* tab = ctx->tab.p + b * tstride;
+    KeyDesc kr = kd;
+    kr.n = nr;
+    if (kd.offsets) kr.offsets = kd.offsets + r0;
+    else kr.bytes = kd.bytes + r0 * kd.key_len;
+    if (pipe && r >= static_cast<uint64_t>(nbuf)) DLSM_TRY(hipStreamWaitEvent(ps, ctx->ev_free[b], 0));
+    DLSM_TRY(launch_probe_mpartition(kr, fs->d_mg, G, rowlen, fs->mg_region, fs->mg_stage_bytes, ent, pos, tab,
+                                     mode, ps));
+    if (pipe) DLSM_CHECK(hand_over(ps, s, ctx->ev_part[b]));
+    for (const MGClass& cl : fs->mg_classes)
+      DLSM_TRY(launch_probe_mslices(cl.lgw, cl.K, fs->d_mg, G, cl.s0, cl.S, rowlen, fs->mg_region, fs->mg_abytes,
+                                    static_cast<uint32_t>(nC), ent, tab, ans, fs->d_mgplan + cl.plan_off, cl.wgs, s));
+    DLSM_TRY(launch_probe_munpermute(nr, fs->d_mg, G, fs->mg_abytes, pos, ans, mask_dev + r0 * mbytes, mbytes, s));
+    if (pipe) DLSM_TRY(hipEventRecord(ctx->ev_free[b], s));
+  }
   return DLSM_OK;
 }
 

@@ -194,3 +194,41 @@ def test_group_with_256_slices(gpu, orc):
     # slices of 256 lines (the most a group may have), beside a packed single
     sizes = [3_350_000] * 8 + [100_000]
     _check(gpu, orc, _filters(orc, sizes), 400_001, 22)
+
+
+@pytest.mark.parametrize("serial", [False, True])
+def test_rounds(gpu, orc, serial):
+    """DLSM_OPT_PROBE_ROUND_KEYS: the batch in rounds (the last one ragged),
+    pipelined over two streams or one after another; 20-byte, hashed and
+    variable-length lookups, against the oracle."""
+    import torch
+
+    import dlsm_amd
+
+    filters = _filters(orc, SHAPES["mixed_8"])
+    gpu.set_probe_round(300_000)
+    gpu.set_probe_serial(serial)
+    try:
+        _check(gpu, orc, filters, 1_000_003, 23)
+        nq = 700_001
+        q = orc.keys_from_values(orc.mt_values(24, 16 * 3_000_000, nq))
+        want = orc.full_probe(filters, q, nq, nthreads=8)
+        h = torch.from_numpy(dlsm_amd.hash_batch(dlsm_amd.Keys(q, nq, 20)).view(np.int32).copy()).cuda()
+        fs = gpu.filterset(filters)
+        try:
+            m = torch.full((nq,), 0x5A, dtype=torch.uint8, device="cuda")
+            gpu.full_probe_hashed_dev(fs, h, m, nq)
+            gpu.sync()
+            assert np.array_equal(m.cpu().numpy(), want)
+            rng = np.random.default_rng(25)
+            keys = [bytes(rng.integers(0, 256, size=int(rng.integers(0, 40)), dtype=np.uint8))
+                    for _ in range(400_001)]
+            data, offs = orc.pack_var(keys)
+            got = gpu.full_probe(fs, dlsm_amd.Keys(np.concatenate([data, np.zeros(16, np.uint8)]), len(keys), 0,
+                                                   offs))
+            assert np.array_equal(got, orc.full_probe(filters, data, len(keys), stride=0, offsets=offs))
+        finally:
+            fs.close()
+    finally:
+        gpu.set_probe_round(0)
+        gpu.set_probe_serial(False)
