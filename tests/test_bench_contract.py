@@ -32,6 +32,13 @@ def test_traffic_summary_matches_default_config():
     assert b.load_traffic(path, dict(cfg, lookups=12_500_000), "probe") is None
     src = json.load(open(path))["source"]
     assert src.startswith("profiles/")
+    # every leg the bench line reports traffic for has its own PMC record
+    for leg in ("legacy", "version", "mixed_set", "dedup_shifted", "block"):
+        rec = b.load_traffic(path, cfg, leg)
+        assert rec is not None and rec["traffic_bytes"] > 0, leg
+    # the sealed block build moves the plain build's bytes (the crc reads LDS)
+    blk = b.load_traffic(path, cfg, "block")
+    assert 0.95 <= blk["traffic_bytes"] / build["traffic_bytes"] <= 1.1
 
 
 def test_host_cores_positive():
