@@ -1012,12 +1012,17 @@ __device__ __forceinline__ uint32_t crc_seal_fold(const uint32_t* part, uint32_t
 }
 // Run the register through the trailer (k, Fixed32 L) and the type byte (0);
 // append [type 0][crc32c::Mask(value)] at `t` (table/table_builder_computeside.cc:418-428).
-__device__ __forceinline__ void crc_seal_append(uint8_t* t, uint32_t r, uint32_t L, int k, const uint32_t* T) {
+__device__ __forceinline__ void crc_seal_append(uint8_t* t, uint32_t r, uint32_t L, int k) {
   const uint8_t tail[6] = {static_cast<uint8_t>(static_cast<int8_t>(k)), static_cast<uint8_t>(L),
                            static_cast<uint8_t>(L >> 8), static_cast<uint8_t>(L >> 16),
                            static_cast<uint8_t>(L >> 24), 0u};
+  // bit by bit: six table lookups would be six dependent global loads
 #pragma unroll
-  for (int b = 0; b < 6; b++) r = (r >> 8) ^ T[(r ^ tail[b]) & 0xffu];
+  for (int b = 0; b < 6; b++) {
+    r ^= tail[b];
+#pragma unroll
+    for (int i = 0; i < 8; i++) r = (r >> 1) ^ (0x82f63b78u & (0u - (r & 1u)));
+  }
   const uint32_t value = ~r;
   const uint32_t m = ((value >> 15) | (value << 17)) + 0xa282ead8u;  // crc32c::Mask
   t[0] = 0;  // kNoCompression
@@ -1205,7 +1210,7 @@ __global__ __launch_bounds__(kSliceBlock) void full_slice_kernel(
       const uint32_t r = crc_seal_fold<R>(crc_part + J.slice0, L, crc_tabs, wsum);
       if (tid == 0) {
         write_trailer(J.out, L, J.k);
-        crc_seal_append(J.out + len, r, L, J.k, crc_tabs);
+        crc_seal_append(J.out + len, r, L, J.k);
         *J.out_len = len + 5u;
         crc_cnt[sj] = 0;
       }
@@ -1239,10 +1244,15 @@ __global__ __launch_bounds__(256) void full_block_seal_kernel(const FullJobDev* 
   if (len == 0) return;
   const uint32_t L = static_cast<uint32_t>((len - 5u) / 64u);
   const uint32_t S = (L + R - 1u) / R;  // slices holding bytes (a lowered L uses fewer)
-  const uint32_t* T = crc_tabs;
   const uint32_t* P1 = crc_tabs + 1024 + kSliceBlock;  // x^(8 * R * 64 * m)
   const uint32_t* P64 = P1 + 256;                     // x^(8 * 64 * m)
   const uint32_t* part = crc_part + J.slice0;
+  // thread 0's last-slice operands, loaded beside the other threads' partials
+  uint32_t p_last = 0, last_part = 0;
+  if (threadIdx.x == 0 && S != 0) {
+    p_last = P64[L - (S - 1u) * R];
+    last_part = part[S - 1u];
+  }
   uint32_t x = 0;  // slices 0 .. S-2, each shifted to the end of slice S-2
   for (uint32_t t = threadIdx.x; t + 1u < S; t += 256u) x ^= crc_mulmod(part[t], P1[S - 2u - t]);
 #pragma unroll
@@ -1252,11 +1262,8 @@ __global__ __launch_bounds__(256) void full_block_seal_kernel(const FullJobDev* 
   if (threadIdx.x != 0) return;
   x = wx[0] ^ wx[1] ^ wx[2] ^ wx[3];
   uint32_t r = 0xffffffffu;  // no lines (an empty filter): the trailer's first byte starts the crc
-  if (S != 0) {
-    const uint32_t nl_last = L - (S - 1u) * R;
-    r = crc_mulmod(x, P64[nl_last]) ^ part[S - 1u];  // after the last slice's lines
-  }
-  crc_seal_append(J.out + len, r, L, J.k, T);
+  if (S != 0) r = crc_mulmod(x, p_last) ^ last_part;  // after the last slice's lines
+  crc_seal_append(J.out + len, r, L, J.k);
   *J.out_len = len + 5u;
 }
 
