@@ -68,7 +68,8 @@ def probe_case(ctx, seed):
 
 def build_case(ctx, seed):
     """A batch of 1-24 tables of 0-200 K keys (duplicates included), one
-    bits_per_key, one key length: full and legacy filters byte-equal."""
+    bits_per_key, one key length: full and legacy filters and sealed filter
+    blocks byte-equal."""
     rng = np.random.default_rng(30_000 + seed)
     T = int(rng.integers(1, 25))
     key_len = int(rng.choice([16, 20, 24, 28, 33]))
@@ -85,7 +86,10 @@ def build_case(ctx, seed):
     ok = all(g == oracle.full_build(t, n, stride=key_len, bpk=bpk) for g, t, n in zip(got, tabs, ns))
     lg = ctx.legacy_build([dlsm_amd.Keys(t, n, key_len) for t, n in zip(tabs, ns)], bpk)
     ok_l = all(g == oracle.legacy_build(t, n, stride=key_len, bpk=bpk) for g, t, n in zip(lg, tabs, ns))
-    return ok and ok_l, T
+    # the same batch as sealed filter blocks (crc32c fused into the slice pass)
+    blk = ctx.full_build_block([dlsm_amd.Keys(t, n, key_len) for t, n in zip(tabs, ns)], bpk)
+    ok_b = all(b == oracle.filter_block(g) for b, g in zip(blk, got))
+    return ok and ok_l and ok_b, T
 
 
 def varlen_keys(rng, vals):
@@ -171,7 +175,7 @@ def main():
         if s % 10 == 9:
             print(f"seed {s + 1}/{seeds}: {len(bad)} mismatches, {time.time() - t0:.0f} s", flush=True)
     ctx.close()
-    print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy),", seeds,
+    print("soak:", seeds, "version cases,", seeds, "probe cases,", seeds, "build batches (full + legacy + sealed blocks),", seeds,
           "variable-length and", seeds, "internal-key build + probe cases, mismatches:",
           bad, flush=True)
     sys.exit(1 if bad else 0)
