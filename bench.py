@@ -1158,9 +1158,11 @@ def block_leg(ctx, stream, tables, bpk, reps=20):
     the crc32c register of each slice's lines from LDS, and one small seal
     kernel folds a filter's slice registers and appends the trailer), against
     the plain batch build on the same stream, HIP events over `reps` calls
-    each.  Algorithmic bytes: 20 B key read + the block written once (the crc
-    reads the filter bytes from LDS, not HBM).  Parity: tests/test_gpu_block_seal.py, tests/test_gpu_parity.py
-    (trailers equal the reference crc32c.cc goldens)."""
+    each, interleaved in groups of 5 (the box's clock drifts over a run).
+    Algorithmic bytes: 20 B key read + the block written once (the crc reads
+    the filter bytes from LDS, not HBM).  Parity: tests/test_gpu_block_seal.py,
+    tests/test_gpu_parity.py (trailers equal the reference crc32c.cc
+    goldens)."""
     import torch
 
     import dlsm_amd
@@ -1171,18 +1173,26 @@ def block_leg(ctx, stream, tables, bpk, reps=20):
         outs = [torch.zeros(dlsm_amd.full_size(t.n)[0] + 64, dtype=torch.uint8, device=dev) for t in tables]
         lens = torch.zeros(T, dtype=torch.uint64, device=dev)
 
-    def timed(fn):
-        fn(tables, outs, lens, bpk)  # warm
+    def timed(fn, n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        for _ in range(reps):
+        for _ in range(n):
             fn(tables, outs, lens, bpk)
         e1.record(stream)
         stream.synchronize()
-        return e0.elapsed_time(e1) / reps
+        return e0.elapsed_time(e1)
 
-    plain = timed(ctx.full_build_dev)
-    block = timed(ctx.full_build_block_dev)
+    ctx.full_build_dev(tables, outs, lens, bpk)  # warm both
+    ctx.full_build_block_dev(tables, outs, lens, bpk)
+    # interleaved groups of 5 calls, so that clock drift over the run falls on
+    # both forms alike
+    plain = block = 0.0
+    groups = max(1, reps // 5)
+    for _ in range(groups):
+        plain += timed(ctx.full_build_dev, 5)
+        block += timed(ctx.full_build_block_dev, 5)
+    plain /= groups * 5
+    block /= groups * 5
     L = lens.cpu().numpy()
     nk = sum(t.n for t in tables)
     alg = nk * 20 + int(L.sum())
