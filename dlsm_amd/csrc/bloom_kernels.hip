@@ -933,41 +933,6 @@ __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
   }
   return p;
 }
-// Compile-time forms for the VALU word step (DLSM_CRC_VALU): x^(8 n) mod P,
-// and the register contribution of each bit after one 4-byte word.
-__host__ __device__ constexpr uint32_t crc_mulmod_c(uint32_t a, uint32_t b) {
-  uint32_t p = 0;
-  for (int i = 0; i < 32; i++) {
-    if (a & (0x80000000u >> i)) p ^= b;
-    b = (b >> 1) ^ ((b & 1u) ? 0x82f63b78u : 0u);
-  }
-  return p;
-}
-__host__ __device__ constexpr uint32_t crc_xpow8_c(uint32_t n) {
-  uint32_t b = 0x80000000u;
-  for (uint32_t i = 0; i < 8u * n; i++) b = (b >> 1) ^ ((b & 1u) ? 0x82f63b78u : 0u);
-  return b;
-}
-struct CrcBitTab {
-  uint32_t c[32];
-  constexpr CrcBitTab() : c{} {
-    for (int b = 0; b < 32; b++) c[b] = crc_mulmod_c(1u << b, crc_xpow8_c(4));
-  }
-};
-constexpr CrcBitTab kCrcBits{};
-#ifndef DLSM_CRC_VALU
-#define DLSM_CRC_VALU 0  // 1: half of each thread's words through a VALU bit step (the other half LDS tables)
-#endif
-// One word through the register with no table: each set bit of (r ^ w) adds
-// its constant (2 VALU per bit: a sign-extended bit field, and-xor).
-__device__ __forceinline__ uint32_t crc_word_valu(uint32_t r, uint32_t w) {
-  const uint32_t x = r ^ w;
-  uint32_t acc = 0;
-#pragma unroll
-  for (int b = 0; b < 32; b++)
-    acc ^= static_cast<uint32_t>(static_cast<int32_t>(x << (31 - b)) >> 31) & kCrcBits.c[b];
-  return acc;
-}
 #ifndef DLSM_CRC_NIB
 #define DLSM_CRC_NIB 1  // slice CRC by 4-bit tables (8 conflict-free lookups / word) instead of byte tables
 #endif
@@ -991,29 +956,17 @@ __device__ __forceinline__ uint32_t crc_slice_partial(const uint32_t* sl, uint32
   static_assert(WPT % 4 == 0, "whole 16-byte reads");
   const uint32_t tid = threadIdx.x;
   const uint32_t padw = (R - nl) * 16u;  // zero words in front (a multiple of 16)
-  // DLSM_CRC_VALU: the first half of the segment through the LDS tables, the
-  // second through the VALU bit step, as two independent registers; the
-  // first is then advanced over the second half's bytes
-  constexpr bool split = DLSM_CRC_VALU && WPT >= 8;
-  uint32_t r = 0, rv = 0;
+  uint32_t r = 0;
 #pragma unroll
   for (uint32_t q = 0; q < WPT / 4; q++) {
     const uint32_t i = tid * WPT + 4u * q;  // first word of this 16-byte piece (padded numbering)
-    const bool valu = split && q >= WPT / 8;
     if (i >= padw) {
       const uint4 v = *reinterpret_cast<const uint4*>(sl + (i - padw));
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-      if (seed && i == padw) (valu ? rv : r) = 0xffffffffu;  // the filter's first byte: crc32c's initial register
+      if (seed && i == padw) r = 0xffffffffu;  // the filter's first byte: crc32c's initial register
 #pragma unroll
-      for (int j = 0; j < 4; j++) {
-        if (valu) rv = crc_word_valu(rv, w4[j]);
-        else r = crc_word(r, w4[j], T);
-      }
+      for (int j = 0; j < 4; j++) r = crc_word(r, w4[j], T);
     }
-  }
-  if constexpr (split) {
-    constexpr uint32_t adv = crc_xpow8_c(2u * WPT);  // the second half's bytes
-    r = crc_mulmod(r, adv) ^ rv;
   }
   r = crc_mulmod(r, shift);  // x^(8 * WPT * 4 * (threads after this one)), loaded at kernel start
 #pragma unroll
